@@ -1,0 +1,158 @@
+/*
+ * yalm_hip.h — the drop-in C ABI of the MI355X (gfx950) decode engine.
+ *
+ * This header replaces the GPU-facing interface of the reference
+ * (/root/reference/src/model.h:33-39, 70-79, 353-385 and the C++ members
+ * compiled in src/infer.cu). It contains no HIP, CUDA or C++ types: every
+ * entry point takes plain pointers, sizes and POD structs, so the reference's
+ * own host (model.cpp, main.cpp, test.cpp) — or our C++20 mirror of it under
+ * yalm_amd/host/ — binds it directly.
+ *
+ * Errors: every int-returning function returns YALM_OK (0) or a YALM_ERR_*
+ * code; yalm_last_error() describes the last failure on the calling thread.
+ * (The reference aborts on any runtime error, infer.cu:13-31; callers that
+ * want that behaviour check the code and abort.)
+ *
+ * Threading: one decoder per stream; a decoder is not re-entrant (same as the
+ * reference's InferenceState, model.h:84-190).
+ */
+#ifndef YALM_HIP_H
+#define YALM_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define YALM_OK 0
+#define YALM_ERR_HIP 1         /* a HIP runtime call failed */
+#define YALM_ERR_ARG 2         /* bad argument / shape */
+#define YALM_ERR_UNSUPPORTED 3 /* configuration the kernels do not implement */
+
+/* DType codes follow the reference enum order (codec.h:15-25). */
+enum { YALM_F32 = 0, YALM_F16 = 1, YALM_BF16 = 2, YALM_F8E5M2 = 3 };
+/* ActivationType (model.h:14-17) */
+enum { YALM_GELU = 0, YALM_SILU = 1 };
+/* InferenceMode (model.h:28-31) */
+enum { YALM_HYDRATE_KV_CACHE = 0, YALM_OUTPUT_LOGITS = 1 };
+
+/* Opaque stream handle; replaces cudaStream_t in init_cuda_stream (model.h:39). */
+typedef struct yalm_stream_s *yalm_stream;
+/* Opaque decoder: the device half of InferenceState + Model (model.h:84-190,
+ * 303-327) — scratch buffers, KV caches, per-mode hipGraphs. */
+typedef struct yalm_decoder_s *yalm_decoder;
+
+/* Config (model.h:41-68). Same field meaning; MoE fields are not carried
+ * because the reference GPU path asserts on MoE (infer.cu:865-867). */
+typedef struct yalm_config {
+	int dim, hidden_dim, head_dim, n_layers, n_heads, n_kv_heads, vocab_size, max_seq_len;
+	float rope_theta;
+	int rotary_dim;
+	float norm_eps;
+	int act;          /* YALM_GELU / YALM_SILU */
+	float qkv_clip;   /* FLT_MAX when absent (model.cpp:60-61) */
+	int weight_dtype; /* YALM_F32 / YALM_F16 / YALM_F8E5M2 */
+} yalm_config;
+
+/* Device pointers of one block (Block private fields, model.h:286-300). If
+ * key_cache/value_cache are NULL the decoder allocates them (zeroed,
+ * max_seq_len x n_kv_heads x head_dim f16 each). */
+typedef struct yalm_block_weights {
+	const float *rms_att, *rms_ffn;
+	const void *wq, *wk, *wv, *wo, *w1, *w2, *w3;
+	uint16_t *key_cache, *value_cache;
+} yalm_block_weights;
+
+/* Device pointers of the model (Model fields, model.h:303-311). wcls may equal
+ * token_embedding (tied weights, model.cpp:370-377). blocks is a HOST array
+ * of n_layers entries, copied by yalm_decoder_create. */
+typedef struct yalm_model_weights {
+	const void *token_embedding;
+	const float *rms_final;
+	const void *wcls;
+	const yalm_block_weights *blocks;
+} yalm_model_weights;
+
+/* ---------------- device shim: replaces model.h:33-39 / infer.cu:59-90 ---------------- */
+const char *yalm_last_error(void);
+/* set_cuda_device (model.h:38): selects the HIP device for this thread. */
+int yalm_set_device(int device);
+/* upload_cuda (model.h:33): device alloc + H2D copy; returns NULL on failure. */
+void *yalm_upload(const void *host, size_t size);
+/* device alloc (zero-filled); returns NULL on failure. */
+void *yalm_alloc(size_t size);
+/* download_cuda (model.h:34): D2H copy into a caller buffer (the reference
+ * allocated pinned memory and passed std::string through extern "C"). */
+int yalm_download(void *host, const void *device, size_t size);
+/* register_cuda_host / unregister_cuda_host (model.h:35, 37). */
+int yalm_register_host(void *host, size_t size);
+int yalm_unregister_host(void *host);
+/* free_cuda (model.h:36). */
+int yalm_free(void *device);
+/* init_cuda_stream (model.h:39), with an opaque handle. */
+int yalm_stream_create(yalm_stream *out);
+int yalm_stream_destroy(yalm_stream s);
+int yalm_stream_sync(yalm_stream s);
+/* Fill n device elements of dtype with the deterministic synthetic
+ * initialiser (uniform in [offset-scale, offset+scale); f32 adds offset).
+ * Used to build random-weight models of real shapes in HBM without a PCIe
+ * upload (bench.py). Same integer hash as the CPU oracle. */
+int yalm_synth(void *device, size_t n, int dtype, uint64_t seed, float scale, float offset, yalm_stream s);
+
+/* ---------------- decoder: replaces Model::_forward_cuda / Block::_block_cuda ---------------- */
+/* Creates the device state for one sequence (InferenceState::cuda,
+ * model.cpp:323-345) on stream s (NULL = a private stream). Weight pointers
+ * must stay valid for the decoder's lifetime. */
+int yalm_decoder_create(const yalm_config *config, const yalm_model_weights *weights, yalm_stream s,
+                        yalm_decoder *out);
+int yalm_decoder_destroy(yalm_decoder d);
+/* Model::forward (model.cpp:396-407 -> infer.cu:1021-1039): one token through
+ * every block at position pos (sliding-window/sink indices as infer.cu:1081-
+ * 1083). mode YALM_OUTPUT_LOGITS also computes the final norm + logits and,
+ * if logits_host != NULL, copies vocab_size floats there before returning
+ * (synchronous, like the reference's OUTPUT mode). YALM_HYDRATE_KV_CACHE is
+ * asynchronous. Graph-replayed after the first call per mode. */
+int yalm_forward(yalm_decoder d, int token, int pos, int mode, float *logits_host);
+/* Device-resident greedy decode (-t 0; sampler.cpp:27-38 first-max argmax on
+ * the device): feeds `token` at `pos`, then n_steps-1 more tokens each chosen
+ * by argmax of the previous step; writes the n_steps argmax tokens to
+ * out_tokens (host). One graph replay per token, no host round trip. */
+int yalm_generate_greedy(yalm_decoder d, int token, int pos, int n_steps, int *out_tokens);
+/* Launch-only variant for benchmarking: enqueue n_steps greedy steps
+ * continuing from the decoder's device-resident token/pos; no sync. */
+int yalm_enqueue_greedy(yalm_decoder d, int n_steps);
+/* Read back the device-resident next token / position after enqueue+sync. */
+int yalm_device_step(yalm_decoder d, int *token, int *pos);
+/* Block::block (model.cpp:213-265) for one layer, eagerly, on the decoder's
+ * current activation x (the test hook for per-layer parity). */
+int yalm_block(yalm_decoder d, int layer, int pos, int kv_sink, int kv_pos, int kv_len);
+/* Host access to the decoder's activation x (dim floats) and logits. */
+int yalm_get_x(yalm_decoder d, float *host);
+int yalm_set_x(yalm_decoder d, const float *host);
+int yalm_get_logits(yalm_decoder d, float *host);
+/* Average device time (ms) of one kernel of the forward, launched eagerly on
+ * the decoder's stream `iters` times between HIP events. kernel_id: 0 = QKV
+ * GEMV, 1 = attention, 2 = Wo GEMV, 3 = W1/W3 GEMV+GLU, 4 = W2 GEMV,
+ * 5 = logits GEMV. Used by bench.py for the roofline of the dominant kernel. */
+int yalm_time_kernel(yalm_decoder d, int kernel_id, int iters, float *avg_ms);
+/* Name of kernel_id's device function (to match rocprofv3 summaries). */
+const char *yalm_kernel_name(yalm_decoder d, int kernel_id);
+
+/* ---------------- test API: replaces infer.cu:890-1019 (model.h:370-384) ---------------- */
+/* Host pointers in and out; synchronous. dtype selects the weight type
+ * (matmul_cuda<float|half|uint8_t>). */
+int yalm_matmul(float *xout, const float *x, const void *w, int n, int d, int dtype);
+/* mha_cuda: xout (n_heads, head_dim), att (n_heads, max_seq_len) softmax
+ * probabilities for t < kv_len. */
+int yalm_mha(float *xout, float *att, const uint16_t *kb, const uint16_t *vb, const float *q, int head_dim, int kv_len,
+             int max_seq_len, int n_heads, int n_kv_heads);
+/* ffn_cuda: xout = W2 (act(W1 x) * W3 x). */
+int yalm_ffn(float *xout, const float *x, const void *w1, const void *w2, const void *w3, int hidden_dim, int dim,
+             int act, int dtype);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,122 @@
+// device_common.h — gfx950 device helpers shared by the decode kernels.
+//
+// Wave64 everywhere (CDNA4): reductions are xor-butterflies over 64 lanes,
+// never the reference's 32-lane warp idioms (infer.cu:110-214).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define YALM_WAVE 64
+
+typedef float float4_t __attribute__((ext_vector_type(4)));
+typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+// Step parameters resident in device memory so that the per-token hipGraph is
+// fully static (no per-node SetParams, unlike infer.cu:1146-1164).
+struct StepState {
+	int token;   // token fed at this step
+	int pos;     // sequence position
+	int kv_sink; // infer.cu:1081
+	int kv_pos;  // infer.cu:1082
+	int kv_len;  // infer.cu:1083
+	int n_gen;   // number of greedy tokens produced so far (device loop)
+	int pad[2];
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+	for (int off = 32; off > 0; off >>= 1)
+		v += __shfl_xor(v, off, 64);
+	return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+	for (int off = 32; off > 0; off >>= 1)
+		v = fmaxf(v, __shfl_xor(v, off, 64));
+	return v;
+}
+
+// Sum over aligned groups of `width` lanes (width a power of two <= 64).
+__device__ __forceinline__ float group_sum(float v, int width) {
+	for (int off = width >> 1; off > 0; off >>= 1)
+		v += __shfl_xor(v, off, 64);
+	return v;
+}
+
+// 16-byte streaming load of weights read exactly once per token: non-temporal
+// (MI355X_MICROARCH.md row nt-weights: decode layers 5-10% faster).
+__device__ __forceinline__ u32x4_t load_nt16(const void *p) {
+	return __builtin_nontemporal_load((const u32x4_t *)p);
+}
+__device__ __forceinline__ u32x4_t load16(const void *p) {
+	return *(const u32x4_t *)p;
+}
+
+__device__ __forceinline__ float h2f(uint16_t h) {
+	_Float16 f;
+	__builtin_memcpy(&f, &h, 2);
+	return (float)f;
+}
+__device__ __forceinline__ uint16_t f2h(float x) { // round to nearest even
+	_Float16 f = (_Float16)x;
+	uint16_t h;
+	__builtin_memcpy(&h, &f, 2);
+	return h;
+}
+
+// Weight element types. EPL = elements per 16-byte lane load.
+struct WF32 {
+	static constexpr int EPL = 4;
+	static constexpr int BYTES = 4;
+	__device__ static __forceinline__ void unpack(const u32x4_t &w, float *o) {
+#pragma unroll
+		for (int i = 0; i < 4; ++i)
+			o[i] = __builtin_bit_cast(float, w[i]);
+	}
+};
+struct WF16 {
+	static constexpr int EPL = 8;
+	static constexpr int BYTES = 2;
+	__device__ static __forceinline__ void unpack(const u32x4_t &w, float *o) {
+#pragma unroll
+		for (int i = 0; i < 4; ++i) {
+			half2_t h = __builtin_bit_cast(half2_t, w[i]);
+			o[2 * i] = (float)h[0];
+			o[2 * i + 1] = (float)h[1];
+		}
+	}
+};
+// OCP E5M2 (== gfx950 "bf8"): the f16 with bits (b << 8), an exact upcast.
+struct WF8 {
+	static constexpr int EPL = 16;
+	static constexpr int BYTES = 1;
+	__device__ static __forceinline__ void unpack(const u32x4_t &w, float *o) {
+#pragma unroll
+		for (int i = 0; i < 4; ++i) {
+			uint32_t v = w[i];
+			// bytes b0..b3 -> f16 pairs (b0<<8 | b1<<24), (b2<<8 | b3<<24)
+			uint32_t lo = ((v & 0xFFu) << 8) | ((v & 0xFF00u) << 16);   // [0, b0, 0, b1]
+			uint32_t hi = ((v & 0xFF0000u) >> 8) | (v & 0xFF000000u); // [0, b2, 0, b3]
+			half2_t a = __builtin_bit_cast(half2_t, lo);
+			half2_t b = __builtin_bit_cast(half2_t, hi);
+			o[4 * i + 0] = (float)a[0];
+			o[4 * i + 1] = (float)a[1];
+			o[4 * i + 2] = (float)b[0];
+			o[4 * i + 3] = (float)b[1];
+		}
+	}
+};
+
+// infer.cu:586-596 semantics (SiLU x/(1+e^-x); GELU tanh approximation).
+template <int ACT>
+__device__ __forceinline__ float act_fn(float x) {
+	if constexpr (ACT == 1) {
+		return x / (1.0f + expf(-x));
+	} else {
+		return 0.5f * x * (1.0f + tanhf(0.797885f * (x + 0.044715f * x * x * x)));
+	}
+}

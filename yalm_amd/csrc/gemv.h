@@ -1,0 +1,279 @@
+// gemv.h — weight-streaming GEMV for batch-1 decode on gfx950.
+//
+// Replaces the reference's warp-per-row GEMVs (infer.cu:216-336, 598-620):
+//   * one wave64 owns a group of R weight rows and streams them with 16-byte
+//     non-temporal loads (U chunks of 64 lanes x 16 B in flight per row),
+//   * the activation vector is staged once per workgroup in LDS as fp32 —
+//     optionally rmsnorm'ed on the way in (fusing infer.cu:526-539 into the
+//     consumer, removing the 1-workgroup norm launch),
+//   * wave64 xor-butterfly reduction, then a per-use epilogue policy:
+//       PStore     out[row]  = acc                 (logits, test matmul, W2 in ffn test)
+//       PResidual  out[row] += acc                 (Wo, W2: fused_matmul_add_residuals)
+//       PQKV       clip + RoPE + fp16 KV-cache write, pairs of rows (fused_qkv_matmul_clip
+//                  + fused_rope_and_cache_update + rotate_sink_tokens)
+//       PGlu       act(W1 row) * (W3 row)          (fused_ffn_w1_w3_glu_act)
+// Accumulation is fp32 (weights widened exactly: f16 -> f32, E5M2 -> f16 -> f32).
+#pragma once
+
+#include "device_common.h"
+
+#define GEMV_THREADS 256
+
+template <class WT, int R_>
+struct PStore {
+	static constexpr int R = R_;
+	const char *W;
+	int n;
+	float *out;
+	int n_groups;
+	__device__ __forceinline__ void prologue() const {}
+	__device__ __forceinline__ const char *row(int g, int r) const {
+		return W + (size_t)(g * R + r) * n * WT::BYTES;
+	}
+	__device__ __forceinline__ void finish(int g, const float *acc, int lane) const {
+		if (lane < R)
+			out[g * R + lane] = acc[lane];
+	}
+};
+
+template <class WT, int R_>
+struct PResidual {
+	static constexpr int R = R_;
+	const char *W;
+	int n;
+	float *out;
+	int n_groups;
+	__device__ __forceinline__ void prologue() const {}
+	__device__ __forceinline__ const char *row(int g, int r) const {
+		return W + (size_t)(g * R + r) * n * WT::BYTES;
+	}
+	__device__ __forceinline__ void finish(int g, const float *acc, int lane) const {
+		if (lane < R)
+			out[g * R + lane] += acc[lane];
+	}
+};
+
+// Virtual row space [wq | wk | wv]; a wave owns the RoPE pair (2g, 2g+1).
+template <class WT>
+struct PQKV {
+	static constexpr int R = 2;
+	const char *wq, *wk, *wv;
+	int n, q_dim, kv_dim, head_dim, n_groups;
+	float qkv_clip;
+	const float *inv_freq; // (head_dim/2) 1/theta^(2j/rotary_dim), 0 past rotary_dim
+	const StepState *step;
+	float *q_out;
+	uint16_t *kcache, *vcache;
+	// workgroup 0 rotates the attention sinks (see rotate_sinks below)
+	__device__ __forceinline__ void prologue() const;
+	__device__ __forceinline__ const char *row(int g, int r) const {
+		int vr = 2 * g + r;
+		if (vr < q_dim)
+			return wq + (size_t)vr * n * WT::BYTES;
+		vr -= q_dim;
+		if (vr < kv_dim)
+			return wk + (size_t)vr * n * WT::BYTES;
+		vr -= kv_dim;
+		return wv + (size_t)vr * n * WT::BYTES;
+	}
+	__device__ __forceinline__ void finish(int g, const float *acc, int lane) const {
+		if (lane != 0)
+			return;
+		// infer.cpp:280-288 clip; infer.cpp:291-301 rope; infer.cu:642-677 cache write
+		float v0 = acc[0] < -qkv_clip ? -qkv_clip : (acc[0] > qkv_clip ? qkv_clip : acc[0]);
+		float v1 = acc[1] < -qkv_clip ? -qkv_clip : (acc[1] > qkv_clip ? qkv_clip : acc[1]);
+		int vr = 2 * g;
+		if (vr >= q_dim + kv_dim) { // V: no rotation
+			size_t o = (size_t)step->kv_pos * kv_dim + (vr - q_dim - kv_dim);
+			vcache[o] = f2h(v0);
+			vcache[o + 1] = f2h(v1);
+			return;
+		}
+		int i = vr < q_dim ? vr : vr - q_dim;
+		float freq = inv_freq[(i % head_dim) >> 1];
+		float val = (float)step->pos * freq;
+		float fcr = cosf(val);
+		float fci = sinf(val);
+		float r0 = v0 * fcr - v1 * fci;
+		float r1 = v0 * fci + v1 * fcr;
+		if (vr < q_dim) {
+			q_out[i] = r0;
+			q_out[i + 1] = r1;
+		} else {
+			size_t o = (size_t)step->kv_pos * kv_dim + i;
+			kcache[o] = f2h(r0);
+			kcache[o + 1] = f2h(r1);
+		}
+	}
+};
+
+template <class WT, int ACT>
+struct PGlu {
+	static constexpr int R = 2;
+	const char *w1, *w3;
+	int n;
+	float *out;
+	int n_groups;
+	__device__ __forceinline__ void prologue() const {}
+	__device__ __forceinline__ const char *row(int g, int r) const {
+		return (r == 0 ? w1 : w3) + (size_t)g * n * WT::BYTES;
+	}
+	__device__ __forceinline__ void finish(int g, const float *acc, int lane) const {
+		if (lane == 0)
+			out[g] = act_fn<ACT>(acc[0]) * acc[1];
+	}
+};
+
+// Rotate the attention-sink keys by one position (infer.cpp:303-317,
+// infer.cu:679-697), executed by workgroup 0 of the QKV launch. Rows < kv_sink
+// never alias the kv_pos row being written (kv_pos >= kv_sink).
+__device__ __forceinline__ void rotate_sinks(uint16_t *kcache, int kv_sink, int kv_dim, int head_dim,
+                                             const float *inv_freq) {
+	for (int r = 0; r < kv_sink; ++r) {
+		for (int i = 2 * threadIdx.x; i < kv_dim; i += 2 * blockDim.x) {
+			size_t o = (size_t)r * kv_dim + i;
+			float v0 = h2f(kcache[o]), v1 = h2f(kcache[o + 1]);
+			float freq = inv_freq[(i % head_dim) >> 1];
+			float val = 1.0f * freq;
+			float fcr = cosf(val), fci = sinf(val);
+			kcache[o] = f2h(v0 * fcr - v1 * fci);
+			kcache[o + 1] = f2h(v0 * fci + v1 * fcr);
+		}
+	}
+}
+
+template <class WT>
+__device__ __forceinline__ void PQKV<WT>::prologue() const {
+	if (blockIdx.x == 0) {
+		const int kv_sink = step->kv_sink;
+		if (kv_sink > 0)
+			rotate_sinks(kcache, kv_sink, kv_dim, head_dim, inv_freq);
+	}
+}
+
+// Stage x (n floats) into LDS, optionally as rmsnorm(x) * w (infer.cpp:134-144
+// statement order: scale = 1/sqrt(sum/n + eps); o = x * scale * w).
+template <bool NORM>
+__device__ __forceinline__ void stage_x(float *xs, const float *__restrict__ x, const float *__restrict__ normw, int n,
+                                        float eps) {
+	const int tid = threadIdx.x;
+	const int nthreads = blockDim.x;
+	float scale = 1.0f;
+	if constexpr (NORM) {
+		float *red = xs + ((n + 3) & ~3); // scratch after x (one aligned LDS region, G17)
+		float ss = 0.0f;
+		for (int i = tid * 4; i < n; i += nthreads * 4) {
+			float4_t v = *(const float4_t *)(x + i);
+			ss += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+		}
+		ss = wave_sum(ss);
+		if ((tid & 63) == 0)
+			red[tid >> 6] = ss;
+		__syncthreads();
+		float tot = 0.0f;
+		for (int w = 0; w < nthreads / YALM_WAVE; ++w)
+			tot += red[w];
+		float rms = sqrtf(tot / n + eps);
+		scale = 1.0f / rms;
+	}
+	for (int i = tid * 4; i < n; i += nthreads * 4) {
+		float4_t v = *(const float4_t *)(x + i);
+		if constexpr (NORM) {
+			float4_t w = *(const float4_t *)(normw + i);
+			v[0] = v[0] * scale * w[0];
+			v[1] = v[1] * scale * w[1];
+			v[2] = v[2] * scale * w[2];
+			v[3] = v[3] * scale * w[3];
+		}
+		*(float4_t *)(xs + i) = v;
+	}
+	__syncthreads();
+}
+
+template <class WT, int R>
+__device__ __forceinline__ void fma_chunk(float (&acc)[R], const u32x4_t (&w)[R], const float *xs_lane) {
+	constexpr int EPL = WT::EPL;
+	float xv[EPL];
+#pragma unroll
+	for (int e = 0; e < EPL; e += 4) {
+		float4_t t = *(const float4_t *)(xs_lane + e);
+		xv[e] = t[0];
+		xv[e + 1] = t[1];
+		xv[e + 2] = t[2];
+		xv[e + 3] = t[3];
+	}
+#pragma unroll
+	for (int r = 0; r < R; ++r) {
+		float wf[EPL];
+		WT::unpack(w[r], wf);
+#pragma unroll
+		for (int e = 0; e < EPL; ++e)
+			acc[r] = fmaf(wf[e], xv[e], acc[r]);
+	}
+}
+
+// n must be a multiple of WT::EPL (the reference asserts n % 16 == 0,
+// infer.cpp:66) and of 4. Each wave processes `gpw` consecutive row groups.
+template <class WT, class P, int U, bool NORM>
+__global__ __launch_bounds__(GEMV_THREADS) void gemv_kernel(P p, const float *__restrict__ x,
+                                                            const float *__restrict__ normw, float eps, int gpw) {
+	extern __shared__ __attribute__((aligned(16))) float xs[];
+	constexpr int R = P::R;
+	constexpr int EPL = WT::EPL;
+	constexpr int CH = YALM_WAVE * EPL; // elements per wave-wide chunk
+	const int n = p.n;
+	p.prologue();
+	stage_x<NORM>(xs, x, normw, n, eps);
+
+	const int lane = threadIdx.x & 63;
+	const int wave = threadIdx.x >> 6;
+	const int waves = blockDim.x >> 6;
+	const int g0 = (blockIdx.x * waves + wave) * gpw;
+	const int nfull = n / CH;
+	const int rem = n - nfull * CH;
+
+	for (int gi = 0; gi < gpw; ++gi) {
+		const int g = g0 + gi;
+		if (g >= p.n_groups)
+			break;
+		const char *rp[R];
+#pragma unroll
+		for (int r = 0; r < R; ++r)
+			rp[r] = p.row(g, r) + (size_t)lane * EPL * WT::BYTES;
+		float acc[R];
+#pragma unroll
+		for (int r = 0; r < R; ++r)
+			acc[r] = 0.0f;
+
+		int c = 0;
+		for (; c + U <= nfull; c += U) {
+			u32x4_t w[U][R];
+#pragma unroll
+			for (int u = 0; u < U; ++u)
+#pragma unroll
+				for (int r = 0; r < R; ++r)
+					w[u][r] = load_nt16(rp[r] + (size_t)(c + u) * CH * WT::BYTES);
+#pragma unroll
+			for (int u = 0; u < U; ++u)
+				fma_chunk<WT, R>(acc, w[u], xs + (c + u) * CH + lane * EPL);
+		}
+		for (; c < nfull; ++c) {
+			u32x4_t w[R];
+#pragma unroll
+			for (int r = 0; r < R; ++r)
+				w[r] = load_nt16(rp[r] + (size_t)c * CH * WT::BYTES);
+			fma_chunk<WT, R>(acc, w, xs + c * CH + lane * EPL);
+		}
+		if (rem > 0 && lane * EPL < rem) {
+			u32x4_t w[R];
+#pragma unroll
+			for (int r = 0; r < R; ++r)
+				w[r] = load_nt16(rp[r] + (size_t)nfull * CH * WT::BYTES);
+			fma_chunk<WT, R>(acc, w, xs + nfull * CH + lane * EPL);
+		}
+#pragma unroll
+		for (int r = 0; r < R; ++r)
+			acc[r] = wave_sum(acc[r]);
+		p.finish(g, acc, lane);
+	}
+}

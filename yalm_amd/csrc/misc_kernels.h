@@ -1,0 +1,126 @@
+// misc_kernels.h — per-token bookkeeping kernels: step setup + embedding row,
+// device argmax (greedy -t 0), and the deterministic synthetic initialiser.
+#pragma once
+
+#include <float.h>
+
+#include "device_common.h"
+
+// Host-provided (token, pos) -> device StepState. Launched eagerly ahead of a
+// graph replay; kernel arguments are captured at launch, so no host buffer race.
+__global__ void set_step_kernel(StepState *st, int token, int pos, int reset_gen) {
+	st->token = token;
+	st->pos = pos;
+	if (reset_gen)
+		st->n_gen = 0;
+}
+
+// Explicit indices for the per-block test hook (Block::block signature).
+__global__ void set_step_full_kernel(StepState *st, int pos, int kv_sink, int kv_pos, int kv_len) {
+	st->pos = pos;
+	st->kv_sink = kv_sink;
+	st->kv_pos = kv_pos;
+	st->kv_len = kv_len;
+}
+
+// First node of every forward graph: sliding-window indices (infer.cu:1081-
+// 1083; KV_SINKS = 2, model.h:12) and x = embedding[token] (infer.cu:622-640).
+template <class WT>
+__global__ __launch_bounds__(256) void step_begin_kernel(StepState *st, const void *__restrict__ emb, int dim,
+                                                         float *__restrict__ x, int max_seq_len) {
+	const int token = st->token;
+	const int pos = st->pos;
+	const char *row = (const char *)emb + (size_t)token * dim * WT::BYTES;
+	for (int i = threadIdx.x * WT::EPL; i < dim; i += blockDim.x * WT::EPL) {
+		float f[WT::EPL];
+		WT::unpack(load16(row + (size_t)i * WT::BYTES), f);
+#pragma unroll
+		for (int e = 0; e < WT::EPL; ++e)
+			x[i + e] = f[e];
+	}
+	if (threadIdx.x == 0) {
+		const int kv_sink = pos >= max_seq_len ? 2 : 0;
+		st->kv_sink = kv_sink;
+		st->kv_pos = kv_sink + (pos - kv_sink) % (max_seq_len - kv_sink);
+		st->kv_len = pos >= max_seq_len ? max_seq_len : pos + 1;
+	}
+}
+
+// Greedy sampling on the device (sampler.cpp:27-38: strict '>' scan, so the
+// FIRST maximum wins). Feeds the result back as the next step's token.
+__global__ __launch_bounds__(1024) void argmax_kernel(const float *__restrict__ logits, int n, StepState *st,
+                                                      int *__restrict__ tokens_out, int cap) {
+	__shared__ float sv[16];
+	__shared__ int si[16];
+	float best = -FLT_MAX;
+	int bi = 0x7fffffff;
+	for (int i = threadIdx.x; i < n; i += blockDim.x) {
+		float v = logits[i];
+		if (v > best) { // ascending i per thread: keeps the first max
+			best = v;
+			bi = i;
+		}
+	}
+	// wave reduce: larger value wins; ties -> smaller index
+#pragma unroll
+	for (int off = 32; off > 0; off >>= 1) {
+		float ov = __shfl_xor(best, off, 64);
+		int oi = __shfl_xor(bi, off, 64);
+		if (ov > best || (ov == best && oi < bi)) {
+			best = ov;
+			bi = oi;
+		}
+	}
+	const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+	if (lane == 0) {
+		sv[wave] = best;
+		si[wave] = bi;
+	}
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		float b = sv[0];
+		int idx = si[0];
+		for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+			if (sv[w] > b || (sv[w] == b && si[w] < idx)) {
+				b = sv[w];
+				idx = si[w];
+			}
+		}
+		if (idx == 0x7fffffff)
+			idx = 0; // all -FLT_MAX / NaN: the reference returns 0
+		const int k = st->n_gen;
+		if (tokens_out && k < cap)
+			tokens_out[k] = idx;
+		st->n_gen = k + 1;
+		st->token = idx;
+		st->pos = st->pos + 1;
+	}
+}
+
+// Deterministic synthetic initialiser — the same integer hash as the CPU
+// oracle (oracle/yalm_oracle.c orc_synth_*), so a random-weight model of a
+// real shape can be built in HBM and reproduced bit-exactly on the host.
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+	x += 0x9E3779B97F4A7C15ull;
+	x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+	x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+	return x ^ (x >> 31);
+}
+
+__global__ void synth_kernel(void *dst, size_t n, int dtype, uint64_t seed, float scale, float offset) {
+	const float k = scale * (1.0f / 8388608.0f);
+	for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+		uint64_t h = splitmix64(seed ^ ((uint64_t)i * 0xD1B54A32D192ED03ull));
+		int32_t s = (int32_t)(h >> 40) - 8388608;
+		if (dtype == 0) {
+			((float *)dst)[i] = __builtin_fmaf((float)s, k, offset);
+		} else {
+			float v = __fmul_rn((float)s, k);
+			uint32_t hb = f2h(v);
+			if (dtype == 1)
+				((uint16_t *)dst)[i] = (uint16_t)hb;
+			else
+				((uint8_t *)dst)[i] = (uint8_t)((hb + 0x7Fu + ((hb >> 8) & 1u)) >> 8);
+		}
+	}
+}

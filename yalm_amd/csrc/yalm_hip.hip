@@ -1,0 +1,810 @@
+// yalm_hip.hip — C ABI (include/yalm_hip.h) of the MI355X decode engine:
+// device shim, decoder (graph-captured per-token forward) and the kernel-level
+// test API. Replaces /root/reference/src/infer.cu:33-90 (shim), 699-888
+// (_block_cuda), 890-1019 (test API), 1021-1164 (_forward_cuda + CudaGraph)
+// and the device upload of model.cpp:185-211, 323-345, 380-394.
+#include "../../include/yalm_hip.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "attention.h"
+#include "device_common.h"
+#include "gemv.h"
+#include "misc_kernels.h"
+
+// ------------------------------------------------------------------ errors
+static thread_local std::string g_err;
+
+static void set_err(const std::string &s) {
+	g_err = s;
+}
+
+#define HIPCHK(expr)                                                                                                   \
+	do {                                                                                                               \
+		hipError_t e_ = (expr);                                                                                        \
+		if (e_ != hipSuccess) {                                                                                        \
+			set_err(std::string(#expr) + " failed: " + hipGetErrorString(e_) + " (" + __FILE__ + ":" +                 \
+			        std::to_string(__LINE__) + ")");                                                                   \
+			return YALM_ERR_HIP;                                                                                       \
+		}                                                                                                              \
+	} while (0)
+
+#define ARGCHK(cond, msg)                                                                                              \
+	do {                                                                                                               \
+		if (!(cond)) {                                                                                                 \
+			set_err(msg);                                                                                              \
+			return YALM_ERR_ARG;                                                                                       \
+		}                                                                                                              \
+	} while (0)
+
+#define TRY(expr)                                                                                                      \
+	do {                                                                                                               \
+		int r_ = (expr);                                                                                               \
+		if (r_ != YALM_OK)                                                                                             \
+			return r_;                                                                                                 \
+	} while (0)
+
+extern "C" const char *yalm_last_error(void) {
+	return g_err.c_str();
+}
+
+// ------------------------------------------------------------------ shim
+extern "C" int yalm_set_device(int device) {
+	HIPCHK(hipSetDevice(device));
+	return YALM_OK;
+}
+
+extern "C" void *yalm_upload(const void *host, size_t size) {
+	void *dev = nullptr;
+	if (hipMalloc(&dev, size ? size : 1) != hipSuccess) {
+		set_err("hipMalloc failed in yalm_upload");
+		return nullptr;
+	}
+	if (size && hipMemcpy(dev, host, size, hipMemcpyHostToDevice) != hipSuccess) {
+		set_err("hipMemcpy H2D failed in yalm_upload");
+		(void)hipFree(dev);
+		return nullptr;
+	}
+	return dev;
+}
+
+extern "C" void *yalm_alloc(size_t size) {
+	void *dev = nullptr;
+	if (hipMalloc(&dev, size ? size : 1) != hipSuccess) {
+		set_err("hipMalloc failed in yalm_alloc");
+		return nullptr;
+	}
+	if (hipMemset(dev, 0, size ? size : 1) != hipSuccess) {
+		set_err("hipMemset failed in yalm_alloc");
+		(void)hipFree(dev);
+		return nullptr;
+	}
+	return dev;
+}
+
+extern "C" int yalm_download(void *host, const void *device, size_t size) {
+	HIPCHK(hipMemcpy(host, device, size, hipMemcpyDeviceToHost));
+	return YALM_OK;
+}
+
+extern "C" int yalm_register_host(void *host, size_t size) {
+	HIPCHK(hipHostRegister(host, size, hipHostRegisterDefault));
+	return YALM_OK;
+}
+
+extern "C" int yalm_unregister_host(void *host) {
+	HIPCHK(hipHostUnregister(host));
+	return YALM_OK;
+}
+
+extern "C" int yalm_free(void *device) {
+	HIPCHK(hipFree(device));
+	return YALM_OK;
+}
+
+extern "C" int yalm_stream_create(yalm_stream *out) {
+	ARGCHK(out, "null stream out");
+	hipStream_t s;
+	HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+	*out = reinterpret_cast<yalm_stream>(s);
+	return YALM_OK;
+}
+
+extern "C" int yalm_stream_destroy(yalm_stream s) {
+	HIPCHK(hipStreamDestroy(reinterpret_cast<hipStream_t>(s)));
+	return YALM_OK;
+}
+
+extern "C" int yalm_stream_sync(yalm_stream s) {
+	HIPCHK(hipStreamSynchronize(reinterpret_cast<hipStream_t>(s)));
+	return YALM_OK;
+}
+
+extern "C" int yalm_synth(void *device, size_t n, int dtype, uint64_t seed, float scale, float offset, yalm_stream s) {
+	ARGCHK(dtype == YALM_F32 || dtype == YALM_F16 || dtype == YALM_F8E5M2, "yalm_synth: bad dtype");
+	hipStream_t st = reinterpret_cast<hipStream_t>(s);
+	synth_kernel<<<4096, 256, 0, st>>>(device, n, dtype, seed, scale, offset);
+	HIPCHK(hipGetLastError());
+	return YALM_OK;
+}
+
+// ------------------------------------------------------------------ launch helpers
+static int gemv_gpw_default() {
+	return 1;
+}
+
+template <class WT, class P, bool NORM>
+static int launch_gemv(const P &p, const float *x, const float *normw, float eps, int gpw, hipStream_t st) {
+	constexpr int U = 4;
+	const int waves = GEMV_THREADS / YALM_WAVE;
+	const int per_block = waves * gpw;
+	const int blocks = (p.n_groups + per_block - 1) / per_block;
+	const size_t lds = (size_t)((p.n + 3) & ~3) * sizeof(float) + 64;
+	auto kern = gemv_kernel<WT, P, U, NORM>;
+	if (lds > 65536) {
+		HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+	}
+	hipLaunchKernelGGL(kern, dim3(blocks), dim3(GEMV_THREADS), lds, st, p, x, normw, eps, gpw);
+	HIPCHK(hipGetLastError());
+	return YALM_OK;
+}
+
+static bool attn_supported(int head_dim, int G) {
+	return (head_dim == 16 || head_dim == 32 || head_dim == 64 || head_dim == 128 || head_dim == 256) && G >= 1 &&
+	       G <= 8;
+}
+
+template <int D>
+static void launch_attn_D(int G, const float *q, const uint16_t *kc, const uint16_t *vc, const StepState *step,
+                          int n_heads, int n_kv, int max_seq_len, int chunk, int nsplit, float *part, float *att,
+                          float *out, hipStream_t st) {
+	dim3 grid(n_kv, nsplit);
+	if (G <= 1)
+		attn_split_kernel<D, 1><<<grid, ATTN_THREADS, 0, st>>>(q, kc, vc, step, n_heads, n_kv, max_seq_len, chunk,
+		                                                       nsplit, part, att);
+	else if (G <= 2)
+		attn_split_kernel<D, 2><<<grid, ATTN_THREADS, 0, st>>>(q, kc, vc, step, n_heads, n_kv, max_seq_len, chunk,
+		                                                       nsplit, part, att);
+	else if (G <= 4)
+		attn_split_kernel<D, 4><<<grid, ATTN_THREADS, 0, st>>>(q, kc, vc, step, n_heads, n_kv, max_seq_len, chunk,
+		                                                       nsplit, part, att);
+	else
+		attn_split_kernel<D, 8><<<grid, ATTN_THREADS, 0, st>>>(q, kc, vc, step, n_heads, n_kv, max_seq_len, chunk,
+		                                                       nsplit, part, att);
+	attn_combine_kernel<D><<<n_heads, 128, 0, st>>>(part, step, chunk, nsplit, max_seq_len, out, att);
+}
+
+static int launch_attn(int head_dim, int n_heads, int n_kv, const float *q, const uint16_t *kc, const uint16_t *vc,
+                       const StepState *step, int max_seq_len, int chunk, int nsplit, float *part, float *att,
+                       float *out, hipStream_t st) {
+	const int G = n_heads / n_kv;
+	switch (head_dim) {
+	case 16:
+		launch_attn_D<16>(G, q, kc, vc, step, n_heads, n_kv, max_seq_len, chunk, nsplit, part, att, out, st);
+		break;
+	case 32:
+		launch_attn_D<32>(G, q, kc, vc, step, n_heads, n_kv, max_seq_len, chunk, nsplit, part, att, out, st);
+		break;
+	case 64:
+		launch_attn_D<64>(G, q, kc, vc, step, n_heads, n_kv, max_seq_len, chunk, nsplit, part, att, out, st);
+		break;
+	case 128:
+		launch_attn_D<128>(G, q, kc, vc, step, n_heads, n_kv, max_seq_len, chunk, nsplit, part, att, out, st);
+		break;
+	case 256:
+		launch_attn_D<256>(G, q, kc, vc, step, n_heads, n_kv, max_seq_len, chunk, nsplit, part, att, out, st);
+		break;
+	default:
+		set_err("unsupported head_dim");
+		return YALM_ERR_UNSUPPORTED;
+	}
+	HIPCHK(hipGetLastError());
+	return YALM_OK;
+}
+
+static int attn_chunk_default() {
+	const char *e = getenv("YALM_ATTN_CHUNK");
+	int c = e ? atoi(e) : 128;
+	if (c < 16)
+		c = 16;
+	if (c > ATTN_MAXCHUNK)
+		c = ATTN_MAXCHUNK;
+	return c;
+}
+
+// ------------------------------------------------------------------ decoder
+enum { GRAPH_HYDRATE = 0, GRAPH_LOGITS = 1, GRAPH_GREEDY = 2, N_GRAPHS = 3 };
+
+struct yalm_decoder_s {
+	yalm_config c{};
+	std::vector<yalm_block_weights> b;
+	const void *emb = nullptr;
+	const float *rms_final = nullptr;
+	const void *wcls = nullptr;
+	hipStream_t stream = nullptr;
+	bool own_stream = false;
+	StepState *step = nullptr;
+	float *x = nullptr, *q = nullptr, *xb2 = nullptr, *hb = nullptr, *part = nullptr, *logits = nullptr,
+	      *inv_freq = nullptr;
+	int *tokens = nullptr;
+	int tokens_cap = 0;
+	float *logits_pinned = nullptr;
+	std::vector<void *> dev_allocs;
+	hipGraph_t graph[N_GRAPHS] = {};
+	hipGraphExec_t exec[N_GRAPHS] = {};
+	int chunk = 128, nsplit = 1;
+	int gpw = 1;
+	std::string kname;
+};
+
+template <class WT>
+static int enqueue_layer_t(yalm_decoder_s *d, int l) {
+	const yalm_config &c = d->c;
+	const yalm_block_weights &w = d->b[l];
+	hipStream_t st = d->stream;
+	const int q_dim = c.n_heads * c.head_dim, kv_dim = c.n_kv_heads * c.head_dim;
+	{
+		PQKV<WT> p;
+		p.wq = (const char *)w.wq;
+		p.wk = (const char *)w.wk;
+		p.wv = (const char *)w.wv;
+		p.n = c.dim;
+		p.q_dim = q_dim;
+		p.kv_dim = kv_dim;
+		p.head_dim = c.head_dim;
+		p.n_groups = (q_dim + 2 * kv_dim) / 2;
+		p.qkv_clip = c.qkv_clip;
+		p.inv_freq = d->inv_freq;
+		p.step = d->step;
+		p.q_out = d->q;
+		p.kcache = w.key_cache;
+		p.vcache = w.value_cache;
+		TRY((launch_gemv<WT, PQKV<WT>, true>(p, d->x, w.rms_att, c.norm_eps, d->gpw, st)));
+	}
+	TRY(launch_attn(c.head_dim, c.n_heads, c.n_kv_heads, d->q, w.key_cache, w.value_cache, d->step, c.max_seq_len,
+	                d->chunk, d->nsplit, d->part, nullptr, d->xb2, st));
+	{
+		PResidual<WT, 1> p;
+		p.W = (const char *)w.wo;
+		p.n = q_dim;
+		p.out = d->x;
+		p.n_groups = c.dim;
+		TRY((launch_gemv<WT, PResidual<WT, 1>, false>(p, d->xb2, nullptr, 0.f, d->gpw, st)));
+	}
+	if (c.act == YALM_SILU) {
+		PGlu<WT, 1> p;
+		p.w1 = (const char *)w.w1;
+		p.w3 = (const char *)w.w3;
+		p.n = c.dim;
+		p.out = d->hb;
+		p.n_groups = c.hidden_dim;
+		TRY((launch_gemv<WT, PGlu<WT, 1>, true>(p, d->x, w.rms_ffn, c.norm_eps, d->gpw, st)));
+	} else {
+		PGlu<WT, 0> p;
+		p.w1 = (const char *)w.w1;
+		p.w3 = (const char *)w.w3;
+		p.n = c.dim;
+		p.out = d->hb;
+		p.n_groups = c.hidden_dim;
+		TRY((launch_gemv<WT, PGlu<WT, 0>, true>(p, d->x, w.rms_ffn, c.norm_eps, d->gpw, st)));
+	}
+	{
+		PResidual<WT, 1> p;
+		p.W = (const char *)w.w2;
+		p.n = c.hidden_dim;
+		p.out = d->x;
+		p.n_groups = c.dim;
+		TRY((launch_gemv<WT, PResidual<WT, 1>, false>(p, d->hb, nullptr, 0.f, d->gpw, st)));
+	}
+	return YALM_OK;
+}
+
+template <class WT>
+static int enqueue_logits_t(yalm_decoder_s *d) {
+	const yalm_config &c = d->c;
+	if (c.vocab_size % 2 == 0) {
+		PStore<WT, 2> p;
+		p.W = (const char *)d->wcls;
+		p.n = c.dim;
+		p.out = d->logits;
+		p.n_groups = c.vocab_size / 2;
+		return launch_gemv<WT, PStore<WT, 2>, true>(p, d->x, d->rms_final, c.norm_eps, d->gpw, d->stream);
+	}
+	PStore<WT, 1> p;
+	p.W = (const char *)d->wcls;
+	p.n = c.dim;
+	p.out = d->logits;
+	p.n_groups = c.vocab_size;
+	return launch_gemv<WT, PStore<WT, 1>, true>(p, d->x, d->rms_final, c.norm_eps, d->gpw, d->stream);
+}
+
+template <class WT>
+static int enqueue_begin_t(yalm_decoder_s *d) {
+	step_begin_kernel<WT><<<1, 256, 0, d->stream>>>(d->step, d->emb, d->c.dim, d->x, d->c.max_seq_len);
+	HIPCHK(hipGetLastError());
+	return YALM_OK;
+}
+
+#define DISPATCH_WT(dtype, FN, ...)                                                                                    \
+	((dtype) == YALM_F32   ? FN<WF32>(__VA_ARGS__)                                                                     \
+	 : (dtype) == YALM_F16 ? FN<WF16>(__VA_ARGS__)                                                                     \
+	                       : FN<WF8>(__VA_ARGS__))
+
+static int enqueue_forward(yalm_decoder_s *d, int which) {
+	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_begin_t, d));
+	for (int l = 0; l < d->c.n_layers; ++l)
+		TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_layer_t, d, l));
+	if (which == GRAPH_HYDRATE)
+		return YALM_OK;
+	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_logits_t, d));
+	if (which == GRAPH_LOGITS) {
+		HIPCHK(hipMemcpyAsync(d->logits_pinned, d->logits, sizeof(float) * d->c.vocab_size, hipMemcpyDeviceToHost,
+		                      d->stream));
+	} else {
+		argmax_kernel<<<1, 1024, 0, d->stream>>>(d->logits, d->c.vocab_size, d->step, d->tokens, d->tokens_cap);
+		HIPCHK(hipGetLastError());
+	}
+	return YALM_OK;
+}
+
+static int ensure_graph(yalm_decoder_s *d, int which) {
+	if (d->exec[which])
+		return YALM_OK;
+	HIPCHK(hipStreamBeginCapture(d->stream, hipStreamCaptureModeRelaxed));
+	int r = enqueue_forward(d, which);
+	hipGraph_t g = nullptr;
+	hipError_t e = hipStreamEndCapture(d->stream, &g);
+	if (r != YALM_OK)
+		return r;
+	HIPCHK(e);
+	d->graph[which] = g;
+	HIPCHK(hipGraphInstantiate(&d->exec[which], g, nullptr, nullptr, 0));
+	return YALM_OK;
+}
+
+static int validate_config(const yalm_config *c) {
+	ARGCHK(c->dim > 0 && c->hidden_dim > 0 && c->n_layers > 0 && c->n_heads > 0 && c->n_kv_heads > 0 &&
+	           c->vocab_size > 0 && c->max_seq_len > 2,
+	       "config: non-positive dimension");
+	ARGCHK(c->n_heads % c->n_kv_heads == 0, "config: n_heads % n_kv_heads != 0");
+	ARGCHK(c->weight_dtype == YALM_F32 || c->weight_dtype == YALM_F16 || c->weight_dtype == YALM_F8E5M2,
+	       "config: weight_dtype must be F32, F16 or F8E5M2");
+	ARGCHK(c->dim % 16 == 0 && c->hidden_dim % 16 == 0 && (c->n_heads * c->head_dim) % 16 == 0,
+	       "config: dim, hidden_dim and n_heads*head_dim must be multiples of 16 (infer.cpp:66)");
+	ARGCHK(c->rotary_dim <= c->head_dim && c->rotary_dim % 2 == 0, "config: bad rotary_dim");
+	if (!attn_supported(c->head_dim, c->n_heads / c->n_kv_heads)) {
+		set_err("config: attention kernel needs head_dim in {16,32,64,128,256} and n_heads/n_kv_heads <= 8");
+		return YALM_ERR_UNSUPPORTED;
+	}
+	return YALM_OK;
+}
+
+static void destroy_decoder(yalm_decoder_s *d) {
+	for (int i = 0; i < N_GRAPHS; ++i) {
+		if (d->exec[i])
+			(void)hipGraphExecDestroy(d->exec[i]);
+		if (d->graph[i])
+			(void)hipGraphDestroy(d->graph[i]);
+	}
+	for (void *p : d->dev_allocs)
+		(void)hipFree(p);
+	if (d->logits_pinned)
+		(void)hipHostFree(d->logits_pinned);
+	if (d->own_stream && d->stream)
+		(void)hipStreamDestroy(d->stream);
+	delete d;
+}
+
+static int dalloc(yalm_decoder_s *d, void **p, size_t bytes) {
+	HIPCHK(hipMalloc(p, bytes ? bytes : 4));
+	d->dev_allocs.push_back(*p);
+	HIPCHK(hipMemset(*p, 0, bytes ? bytes : 4));
+	return YALM_OK;
+}
+
+extern "C" int yalm_decoder_create(const yalm_config *config, const yalm_model_weights *weights, yalm_stream s,
+                                   yalm_decoder *out) {
+	ARGCHK(config && weights && out && weights->blocks, "yalm_decoder_create: null argument");
+	TRY(validate_config(config));
+	yalm_decoder_s *d = new yalm_decoder_s();
+	d->c = *config;
+	d->emb = weights->token_embedding;
+	d->rms_final = weights->rms_final;
+	d->wcls = weights->wcls;
+	d->b.assign(weights->blocks, weights->blocks + config->n_layers);
+	int r = YALM_OK;
+	auto fail = [&](int code) {
+		destroy_decoder(d);
+		return code;
+	};
+	if (s) {
+		d->stream = reinterpret_cast<hipStream_t>(s);
+	} else {
+		if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) {
+			set_err("hipStreamCreate failed");
+			return fail(YALM_ERR_HIP);
+		}
+		d->own_stream = true;
+	}
+	const yalm_config &c = d->c;
+	const int q_dim = c.n_heads * c.head_dim, kv_dim = c.n_kv_heads * c.head_dim;
+	d->chunk = attn_chunk_default();
+	d->nsplit = (c.max_seq_len + d->chunk - 1) / d->chunk;
+	d->tokens_cap = 1 << 16;
+	const char *g = getenv("YALM_GEMV_GPW");
+	d->gpw = g ? atoi(g) : gemv_gpw_default();
+	if (d->gpw < 1)
+		d->gpw = 1;
+	if ((r = dalloc(d, (void **)&d->step, sizeof(StepState))) || (r = dalloc(d, (void **)&d->x, sizeof(float) * c.dim)) ||
+	    (r = dalloc(d, (void **)&d->q, sizeof(float) * q_dim)) ||
+	    (r = dalloc(d, (void **)&d->xb2, sizeof(float) * q_dim)) ||
+	    (r = dalloc(d, (void **)&d->hb, sizeof(float) * c.hidden_dim)) ||
+	    (r = dalloc(d, (void **)&d->part, sizeof(float) * (size_t)c.n_heads * d->nsplit * (c.head_dim + 2))) ||
+	    (r = dalloc(d, (void **)&d->logits, sizeof(float) * c.vocab_size)) ||
+	    (r = dalloc(d, (void **)&d->inv_freq, sizeof(float) * c.head_dim / 2)) ||
+	    (r = dalloc(d, (void **)&d->tokens, sizeof(int) * d->tokens_cap)))
+		return fail(r);
+	// RoPE frequencies on the host with the CPU oracle's expression
+	// (infer.cpp:203): 1/powf(theta, j/rotary_dim) for even j < rotary_dim, else 0.
+	std::vector<float> inv(c.head_dim / 2);
+	for (int j = 0; j < c.head_dim; j += 2)
+		inv[j / 2] = j >= c.rotary_dim ? 0.f : 1.0f / powf(c.rope_theta, (float)j / (float)c.rotary_dim);
+	if (hipMemcpy(d->inv_freq, inv.data(), sizeof(float) * inv.size(), hipMemcpyHostToDevice) != hipSuccess) {
+		set_err("inv_freq upload failed");
+		return fail(YALM_ERR_HIP);
+	}
+	for (auto &bw : d->b) {
+		const size_t kvb = sizeof(uint16_t) * (size_t)c.max_seq_len * kv_dim;
+		if (!bw.key_cache && (r = dalloc(d, (void **)&bw.key_cache, kvb)))
+			return fail(r);
+		if (!bw.value_cache && (r = dalloc(d, (void **)&bw.value_cache, kvb)))
+			return fail(r);
+	}
+	if (hipHostMalloc((void **)&d->logits_pinned, sizeof(float) * c.vocab_size, hipHostMallocDefault) != hipSuccess) {
+		set_err("hipHostMalloc failed");
+		return fail(YALM_ERR_HIP);
+	}
+	if (hipDeviceSynchronize() != hipSuccess) {
+		set_err("hipDeviceSynchronize failed after decoder allocation");
+		return fail(YALM_ERR_HIP);
+	}
+	*out = d;
+	return YALM_OK;
+}
+
+extern "C" int yalm_decoder_destroy(yalm_decoder d) {
+	if (!d)
+		return YALM_OK;
+	(void)hipStreamSynchronize(d->stream);
+	destroy_decoder(d);
+	return YALM_OK;
+}
+
+extern "C" int yalm_forward(yalm_decoder d, int token, int pos, int mode, float *logits_host) {
+	ARGCHK(d, "null decoder");
+	ARGCHK(token >= 0 && token < d->c.vocab_size, "token out of range");
+	ARGCHK(pos >= 0, "negative pos");
+	const int which = mode == YALM_HYDRATE_KV_CACHE ? GRAPH_HYDRATE : GRAPH_LOGITS;
+	TRY(ensure_graph(d, which));
+	set_step_kernel<<<1, 1, 0, d->stream>>>(d->step, token, pos, 0);
+	HIPCHK(hipGetLastError());
+	HIPCHK(hipGraphLaunch(d->exec[which], d->stream));
+	if (which == GRAPH_LOGITS) {
+		HIPCHK(hipStreamSynchronize(d->stream));
+		if (logits_host)
+			memcpy(logits_host, d->logits_pinned, sizeof(float) * d->c.vocab_size);
+	}
+	return YALM_OK;
+}
+
+extern "C" int yalm_enqueue_greedy(yalm_decoder d, int n_steps) {
+	ARGCHK(d, "null decoder");
+	TRY(ensure_graph(d, GRAPH_GREEDY));
+	for (int i = 0; i < n_steps; ++i)
+		HIPCHK(hipGraphLaunch(d->exec[GRAPH_GREEDY], d->stream));
+	return YALM_OK;
+}
+
+extern "C" int yalm_generate_greedy(yalm_decoder d, int token, int pos, int n_steps, int *out_tokens) {
+	ARGCHK(d && out_tokens, "null argument");
+	ARGCHK(token >= 0 && token < d->c.vocab_size && pos >= 0 && n_steps >= 0, "bad token/pos/n_steps");
+	TRY(ensure_graph(d, GRAPH_GREEDY));
+	int done = 0;
+	bool first = true;
+	while (done < n_steps) {
+		const int batch = std::min(n_steps - done, d->tokens_cap);
+		if (first)
+			set_step_kernel<<<1, 1, 0, d->stream>>>(d->step, token, pos, 1);
+		else
+			set_step_kernel<<<1, 1, 0, d->stream>>>(d->step, out_tokens[done - 1], pos + done, 1);
+		HIPCHK(hipGetLastError());
+		first = false;
+		for (int i = 0; i < batch; ++i)
+			HIPCHK(hipGraphLaunch(d->exec[GRAPH_GREEDY], d->stream));
+		HIPCHK(hipMemcpyAsync(out_tokens + done, d->tokens, sizeof(int) * batch, hipMemcpyDeviceToHost, d->stream));
+		HIPCHK(hipStreamSynchronize(d->stream));
+		done += batch;
+	}
+	return YALM_OK;
+}
+
+extern "C" int yalm_device_step(yalm_decoder d, int *token, int *pos) {
+	ARGCHK(d, "null decoder");
+	StepState s;
+	HIPCHK(hipStreamSynchronize(d->stream));
+	HIPCHK(hipMemcpy(&s, d->step, sizeof(s), hipMemcpyDeviceToHost));
+	if (token)
+		*token = s.token;
+	if (pos)
+		*pos = s.pos;
+	return YALM_OK;
+}
+
+extern "C" int yalm_block(yalm_decoder d, int layer, int pos, int kv_sink, int kv_pos, int kv_len) {
+	ARGCHK(d && layer >= 0 && layer < d->c.n_layers, "bad layer");
+	ARGCHK(kv_len >= 1 && kv_len <= d->c.max_seq_len && kv_pos >= 0 && kv_pos < d->c.max_seq_len,
+	       "bad kv indices");
+	set_step_full_kernel<<<1, 1, 0, d->stream>>>(d->step, pos, kv_sink, kv_pos, kv_len);
+	HIPCHK(hipGetLastError());
+	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_layer_t, d, layer));
+	HIPCHK(hipStreamSynchronize(d->stream));
+	return YALM_OK;
+}
+
+extern "C" int yalm_get_x(yalm_decoder d, float *host) {
+	ARGCHK(d && host, "null argument");
+	HIPCHK(hipStreamSynchronize(d->stream));
+	HIPCHK(hipMemcpy(host, d->x, sizeof(float) * d->c.dim, hipMemcpyDeviceToHost));
+	return YALM_OK;
+}
+
+extern "C" int yalm_set_x(yalm_decoder d, const float *host) {
+	ARGCHK(d && host, "null argument");
+	HIPCHK(hipStreamSynchronize(d->stream));
+	HIPCHK(hipMemcpy(d->x, host, sizeof(float) * d->c.dim, hipMemcpyHostToDevice));
+	return YALM_OK;
+}
+
+extern "C" int yalm_get_logits(yalm_decoder d, float *host) {
+	ARGCHK(d && host, "null argument");
+	HIPCHK(hipStreamSynchronize(d->stream));
+	HIPCHK(hipMemcpy(host, d->logits, sizeof(float) * d->c.vocab_size, hipMemcpyDeviceToHost));
+	return YALM_OK;
+}
+
+template <class WT>
+static int enqueue_one_t(yalm_decoder_s *d, int kernel_id, int l) {
+	const yalm_config &c = d->c;
+	const yalm_block_weights &w = d->b[l];
+	const int q_dim = c.n_heads * c.head_dim;
+	switch (kernel_id) {
+	case 0:
+	case 2:
+	case 3:
+	case 4: {
+		// reuse the layer enqueue path for exactly one kernel
+		if (kernel_id == 0) {
+			PQKV<WT> p;
+			p.wq = (const char *)w.wq;
+			p.wk = (const char *)w.wk;
+			p.wv = (const char *)w.wv;
+			p.n = c.dim;
+			p.q_dim = q_dim;
+			p.kv_dim = c.n_kv_heads * c.head_dim;
+			p.head_dim = c.head_dim;
+			p.n_groups = (q_dim + 2 * p.kv_dim) / 2;
+			p.qkv_clip = c.qkv_clip;
+			p.inv_freq = d->inv_freq;
+			p.step = d->step;
+			p.q_out = d->q;
+			p.kcache = w.key_cache;
+			p.vcache = w.value_cache;
+			return launch_gemv<WT, PQKV<WT>, true>(p, d->x, w.rms_att, c.norm_eps, d->gpw, d->stream);
+		}
+		if (kernel_id == 2 || kernel_id == 4) {
+			PResidual<WT, 1> p;
+			p.W = (const char *)(kernel_id == 2 ? w.wo : w.w2);
+			p.n = kernel_id == 2 ? q_dim : c.hidden_dim;
+			p.out = d->x;
+			p.n_groups = c.dim;
+			return launch_gemv<WT, PResidual<WT, 1>, false>(p, kernel_id == 2 ? d->xb2 : d->hb, nullptr, 0.f, d->gpw,
+			                                               d->stream);
+		}
+		PGlu<WT, 1> p;
+		p.w1 = (const char *)w.w1;
+		p.w3 = (const char *)w.w3;
+		p.n = c.dim;
+		p.out = d->hb;
+		p.n_groups = c.hidden_dim;
+		return launch_gemv<WT, PGlu<WT, 1>, true>(p, d->x, w.rms_ffn, c.norm_eps, d->gpw, d->stream);
+	}
+	case 1:
+		return launch_attn(c.head_dim, c.n_heads, c.n_kv_heads, d->q, w.key_cache, w.value_cache, d->step,
+		                   c.max_seq_len, d->chunk, d->nsplit, d->part, nullptr, d->xb2, d->stream);
+	case 5:
+		return enqueue_logits_t<WT>(d);
+	}
+	set_err("bad kernel_id");
+	return YALM_ERR_ARG;
+}
+
+extern "C" int yalm_time_kernel(yalm_decoder d, int kernel_id, int iters, float *avg_ms) {
+	ARGCHK(d && avg_ms && iters > 0 && kernel_id >= 0 && kernel_id <= 5, "bad argument");
+	hipEvent_t e0, e1;
+	HIPCHK(hipEventCreate(&e0));
+	HIPCHK(hipEventCreate(&e1));
+	// warm-up once, then time; rotate layers so weights come from HBM, not the
+	// 256 MiB Infinity Cache.
+	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_one_t, d, kernel_id, 0));
+	HIPCHK(hipEventRecord(e0, d->stream));
+	for (int i = 0; i < iters; ++i)
+		TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_one_t, d, kernel_id, (i + 1) % d->c.n_layers));
+	HIPCHK(hipEventRecord(e1, d->stream));
+	HIPCHK(hipEventSynchronize(e1));
+	float ms = 0.f;
+	HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+	(void)hipEventDestroy(e0);
+	(void)hipEventDestroy(e1);
+	*avg_ms = ms / iters;
+	return YALM_OK;
+}
+
+extern "C" const char *yalm_kernel_name(yalm_decoder d, int kernel_id) {
+	if (!d)
+		return "";
+	const char *wt = d->c.weight_dtype == YALM_F32 ? "WF32" : d->c.weight_dtype == YALM_F16 ? "WF16" : "WF8";
+	std::string s;
+	switch (kernel_id) {
+	case 0:
+		s = std::string("gemv_kernel<") + wt + ", PQKV<";
+		break;
+	case 1:
+		s = "attn_split_kernel<";
+		break;
+	case 2:
+	case 4:
+		s = std::string("gemv_kernel<") + wt + ", PResidual<";
+		break;
+	case 3:
+		s = std::string("gemv_kernel<") + wt + ", PGlu<";
+		break;
+	case 5:
+		s = std::string("gemv_kernel<") + wt + ", PStore<";
+		break;
+	default:
+		s = "";
+	}
+	d->kname = s;
+	return d->kname.c_str();
+}
+
+// ------------------------------------------------------------------ test API (host pointers)
+namespace {
+struct DevBuf {
+	void *p = nullptr;
+	~DevBuf() {
+		if (p)
+			(void)hipFree(p);
+	}
+};
+int up(DevBuf &b, const void *host, size_t bytes) {
+	HIPCHK(hipMalloc(&b.p, bytes ? bytes : 4));
+	if (host)
+		HIPCHK(hipMemcpy(b.p, host, bytes, hipMemcpyHostToDevice));
+	else
+		HIPCHK(hipMemset(b.p, 0, bytes ? bytes : 4));
+	return YALM_OK;
+}
+size_t wbytes(int dtype) {
+	return dtype == YALM_F32 ? 4 : dtype == YALM_F16 ? 2 : 1;
+}
+} // namespace
+
+template <class WT>
+static int matmul_t(float *out, const float *x, const void *w, int n, int d) {
+	PStore<WT, 1> p;
+	p.W = (const char *)w;
+	p.n = n;
+	p.out = out;
+	p.n_groups = d;
+	return launch_gemv<WT, PStore<WT, 1>, false>(p, x, nullptr, 0.f, 1, nullptr);
+}
+
+extern "C" int yalm_matmul(float *xout, const float *x, const void *w, int n, int d, int dtype) {
+	ARGCHK(xout && x && w && n > 0 && d > 0, "bad argument");
+	ARGCHK(dtype == YALM_F32 || dtype == YALM_F16 || dtype == YALM_F8E5M2, "bad dtype");
+	ARGCHK(n % 16 == 0, "n must be a multiple of 16 (infer.cpp:66)");
+	DevBuf dx, dw, dout;
+	TRY(up(dx, x, sizeof(float) * n));
+	TRY(up(dw, w, wbytes(dtype) * (size_t)n * d));
+	TRY(up(dout, nullptr, sizeof(float) * d));
+	TRY(DISPATCH_WT(dtype, matmul_t, (float *)dout.p, (const float *)dx.p, dw.p, n, d));
+	HIPCHK(hipDeviceSynchronize());
+	HIPCHK(hipMemcpy(xout, dout.p, sizeof(float) * d, hipMemcpyDeviceToHost));
+	return YALM_OK;
+}
+
+extern "C" int yalm_mha(float *xout, float *att, const uint16_t *kb, const uint16_t *vb, const float *q, int head_dim,
+                        int kv_len, int max_seq_len, int n_heads, int n_kv_heads) {
+	ARGCHK(xout && kb && vb && q, "null argument");
+	ARGCHK(n_kv_heads > 0 && n_heads % n_kv_heads == 0 && kv_len >= 1 && kv_len <= max_seq_len, "bad shape");
+	if (!attn_supported(head_dim, n_heads / n_kv_heads)) {
+		set_err("unsupported head_dim / group size");
+		return YALM_ERR_UNSUPPORTED;
+	}
+	const size_t kvn = (size_t)max_seq_len * n_kv_heads * head_dim;
+	const int chunk = attn_chunk_default();
+	const int nsplit = (max_seq_len + chunk - 1) / chunk;
+	DevBuf dk, dv, dq, dout, datt, dpart, dstep;
+	TRY(up(dk, kb, kvn * 2));
+	TRY(up(dv, vb, kvn * 2));
+	TRY(up(dq, q, sizeof(float) * n_heads * head_dim));
+	TRY(up(dout, nullptr, sizeof(float) * n_heads * head_dim));
+	TRY(up(datt, att, sizeof(float) * (size_t)n_heads * max_seq_len));
+	TRY(up(dpart, nullptr, sizeof(float) * (size_t)n_heads * nsplit * (head_dim + 2)));
+	TRY(up(dstep, nullptr, sizeof(StepState)));
+	set_step_full_kernel<<<1, 1>>>((StepState *)dstep.p, kv_len - 1, 0, kv_len - 1, kv_len);
+	TRY(launch_attn(head_dim, n_heads, n_kv_heads, (const float *)dq.p, (const uint16_t *)dk.p,
+	                (const uint16_t *)dv.p, (const StepState *)dstep.p, max_seq_len, chunk, nsplit,
+	                (float *)dpart.p, att ? (float *)datt.p : nullptr, (float *)dout.p, nullptr));
+	HIPCHK(hipDeviceSynchronize());
+	HIPCHK(hipMemcpy(xout, dout.p, sizeof(float) * n_heads * head_dim, hipMemcpyDeviceToHost));
+	if (att)
+		HIPCHK(hipMemcpy(att, datt.p, sizeof(float) * (size_t)n_heads * max_seq_len, hipMemcpyDeviceToHost));
+	return YALM_OK;
+}
+
+template <class WT>
+static int ffn_t(float *out, const float *x, const void *w1, const void *w2, const void *w3, float *hb, int hidden,
+                 int dim, int act) {
+	if (act == YALM_SILU) {
+		PGlu<WT, 1> p;
+		p.w1 = (const char *)w1;
+		p.w3 = (const char *)w3;
+		p.n = dim;
+		p.out = hb;
+		p.n_groups = hidden;
+		TRY((launch_gemv<WT, PGlu<WT, 1>, false>(p, x, nullptr, 0.f, 1, nullptr)));
+	} else {
+		PGlu<WT, 0> p;
+		p.w1 = (const char *)w1;
+		p.w3 = (const char *)w3;
+		p.n = dim;
+		p.out = hb;
+		p.n_groups = hidden;
+		TRY((launch_gemv<WT, PGlu<WT, 0>, false>(p, x, nullptr, 0.f, 1, nullptr)));
+	}
+	PStore<WT, 1> p;
+	p.W = (const char *)w2;
+	p.n = hidden;
+	p.out = out;
+	p.n_groups = dim;
+	return launch_gemv<WT, PStore<WT, 1>, false>(p, hb, nullptr, 0.f, 1, nullptr);
+}
+
+extern "C" int yalm_ffn(float *xout, const float *x, const void *w1, const void *w2, const void *w3, int hidden_dim,
+                        int dim, int act, int dtype) {
+	ARGCHK(xout && x && w1 && w2 && w3 && hidden_dim > 0 && dim > 0, "bad argument");
+	ARGCHK(dtype == YALM_F32 || dtype == YALM_F16 || dtype == YALM_F8E5M2, "bad dtype");
+	ARGCHK(dim % 16 == 0 && hidden_dim % 16 == 0, "dims must be multiples of 16");
+	const size_t wb = wbytes(dtype) * (size_t)hidden_dim * dim;
+	DevBuf dx, d1, d2, d3, dhb, dout;
+	TRY(up(dx, x, sizeof(float) * dim));
+	TRY(up(d1, w1, wb));
+	TRY(up(d2, w2, wb));
+	TRY(up(d3, w3, wb));
+	TRY(up(dhb, nullptr, sizeof(float) * hidden_dim));
+	TRY(up(dout, nullptr, sizeof(float) * dim));
+	TRY(DISPATCH_WT(dtype, ffn_t, (float *)dout.p, (const float *)dx.p, d1.p, d2.p, d3.p, (float *)dhb.p, hidden_dim,
+	                dim, act));
+	HIPCHK(hipDeviceSynchronize());
+	HIPCHK(hipMemcpy(xout, dout.p, sizeof(float) * dim, hipMemcpyDeviceToHost));
+	return YALM_OK;
+}

@@ -1,0 +1,265 @@
+"""Model configuration (reference Config, model.h:41-68 / model.cpp:17-75),
+.yalm tensor naming (model.cpp:347-378) and synthetic random-weight models
+of real shapes (there is no network for checkpoints: see DESIGN.md).
+"""
+
+from __future__ import annotations
+
+import dataclasses
+
+import numpy as np
+
+F32, F16, BF16, F8E5M2 = 0, 1, 2, 3
+GELU, SILU = 0, 1
+FLT_MAX = 3.4028234663852886e38
+KV_SINKS = 2  # model.h:12
+
+DTYPE_NAMES = {"fp32": F32, "fp16": F16, "fp8": F8E5M2}
+DTYPE_STRINGS = {F32: "F32", F16: "F16", F8E5M2: "F8_E5M2"}
+DTYPE_BYTES = {F32: 4, F16: 2, F8E5M2: 1}
+
+
+@dataclasses.dataclass
+class ModelConfig:
+    dim: int
+    hidden_dim: int
+    head_dim: int
+    n_layers: int
+    n_heads: int
+    n_kv_heads: int
+    vocab_size: int
+    max_seq_len: int
+    rope_theta: float = 10000.0
+    rotary_dim: int = 0
+    norm_eps: float = 1e-5
+    act: int = SILU
+    qkv_clip: float = FLT_MAX
+    weight_dtype: int = F16
+    tied: bool = False
+    bos_token_id: int = 1
+    eos_token_id: int = 2
+
+    def __post_init__(self):
+        if not self.rotary_dim:
+            self.rotary_dim = self.head_dim
+
+    @property
+    def q_dim(self):
+        return self.n_heads * self.head_dim
+
+    @property
+    def kv_dim(self):
+        return self.n_kv_heads * self.head_dim
+
+    def with_(self, **kw) -> "ModelConfig":
+        return dataclasses.replace(self, **kw)
+
+    def weight_bytes_per_token(self) -> int:
+        """Algorithmic HBM bytes read per decode token, excluding the KV cache
+        (SURVEY.md §8d): every layer's weights + norms, one embedding row, the
+        final norm and the classifier."""
+        wb = DTYPE_BYTES[self.weight_dtype]
+        per_layer = 2 * self.dim * 4
+        per_layer += (self.q_dim + 2 * self.kv_dim) * self.dim * wb  # wq wk wv
+        per_layer += self.dim * self.q_dim * wb  # wo
+        per_layer += 3 * self.dim * self.hidden_dim * wb  # w1 w2 w3
+        return self.n_layers * per_layer + self.dim * wb + self.dim * 4 + self.vocab_size * self.dim * wb
+
+    def kv_bytes_per_token(self, kv_len: int) -> int:
+        """fp16 K and V rows read by attention at kv_len (2 * 2 B * kv_dim per row, per layer)."""
+        return self.n_layers * 2 * 2 * self.kv_dim * kv_len
+
+    def metadata(self) -> dict:
+        """__metadata__ strings as convert.py writes them (convert.py:59-81)."""
+        inv = {v: k for k, v in DTYPE_NAMES.items()}
+        md = {
+            "arch": "MistralForCausalLM",
+            "dtype": inv[self.weight_dtype],
+            "dim": str(self.dim),
+            "hidden_dim": str(self.hidden_dim),
+            "head_dim": str(self.head_dim),
+            "n_layers": str(self.n_layers),
+            "n_heads": str(self.n_heads),
+            "n_kv_heads": str(self.n_kv_heads),
+            "vocab_size": str(self.vocab_size),
+            "max_seq_len": str(self.max_seq_len),
+            "bos_token_id": str(self.bos_token_id),
+            "eos_token_id": str(self.eos_token_id),
+            "rope_theta": str(self.rope_theta),
+            "rotary_dim": str(self.rotary_dim),
+            "norm_eps": str(self.norm_eps),
+            "norm_type": "rmsnorm",
+            "act_type": "silu" if self.act == SILU else "gelu",
+        }
+        if self.qkv_clip != FLT_MAX:
+            md["qkv_clip"] = str(self.qkv_clip)
+        return md
+
+
+def config_from_metadata(md: dict, context: int = 0, tied: bool = False) -> ModelConfig:
+    """Config::from_yalm (model.cpp:17-75)."""
+    dtype = md["dtype"]
+    if dtype not in DTYPE_NAMES:
+        raise ValueError(f"FATAL: unsupported dtype: {dtype}")
+    max_seq_len = min(int(md["max_seq_len"]), 4096)  # model.cpp:33
+    if context:
+        max_seq_len = context
+    act_str = md.get("act_type", "gelu")
+    act = SILU if act_str == "silu" else GELU
+    return ModelConfig(
+        dim=int(md["dim"]),
+        hidden_dim=int(md["hidden_dim"]),
+        head_dim=int(md["head_dim"]),
+        n_layers=int(md["n_layers"]),
+        n_heads=int(md["n_heads"]),
+        n_kv_heads=int(md["n_kv_heads"]),
+        vocab_size=int(md["vocab_size"]),
+        max_seq_len=max_seq_len,
+        rope_theta=float(np.float32(float(md["rope_theta"]))),
+        rotary_dim=int(md["rotary_dim"]),
+        norm_eps=float(np.float32(float(md.get("norm_eps", "1e-5")))),
+        act=act,
+        qkv_clip=float(np.float32(float(md["qkv_clip"]))) if "qkv_clip" in md else FLT_MAX,
+        weight_dtype=DTYPE_NAMES[dtype],
+        tied=tied,
+        bos_token_id=int(md.get("bos_token_id", "1")),
+        eos_token_id=int(md.get("eos_token_id", "2")),
+    )
+
+
+# Real shapes (HF config.json values). Weights are synthetic.
+MISTRAL_7B = ModelConfig(
+    dim=4096, hidden_dim=14336, head_dim=128, n_layers=32, n_heads=32, n_kv_heads=8, vocab_size=32000,
+    max_seq_len=4096, rope_theta=1e6, norm_eps=1e-5, act=SILU, weight_dtype=F16, tied=False,
+)
+LLAMA_32_3B = ModelConfig(
+    dim=3072, hidden_dim=8192, head_dim=128, n_layers=28, n_heads=24, n_kv_heads=8, vocab_size=128256,
+    max_seq_len=4096, rope_theta=5e5, norm_eps=1e-5, act=SILU, weight_dtype=F16, tied=True,
+)
+TINY = ModelConfig(
+    dim=64, hidden_dim=128, head_dim=16, n_layers=2, n_heads=4, n_kv_heads=2, vocab_size=384, max_seq_len=64,
+    rope_theta=10000.0, act=SILU, weight_dtype=F16,
+)
+SMALL = ModelConfig(
+    dim=512, hidden_dim=1536, head_dim=64, n_layers=4, n_heads=8, n_kv_heads=2, vocab_size=2048, max_seq_len=256,
+    rope_theta=10000.0, act=SILU, weight_dtype=F16,
+)
+PRESETS = {"mistral-7b": MISTRAL_7B, "llama-3.2-3b": LLAMA_32_3B, "tiny": TINY, "small": SMALL}
+
+
+def layer_names(l: int) -> dict:
+    p = f"model.layers.{l}."
+    return {
+        "rms_att": p + "attn.norm.weight",
+        "rms_ffn": p + "mlp.norm.weight",
+        "wq": p + "attn.wq.weight",
+        "wk": p + "attn.wk.weight",
+        "wv": p + "attn.wv.weight",
+        "wo": p + "attn.wo.weight",
+        "w1": p + "mlp.w1.weight",
+        "w2": p + "mlp.w2.weight",
+        "w3": p + "mlp.w3.weight",
+    }
+
+
+def tensor_shapes(c: ModelConfig) -> dict:
+    """name -> (shape, is_norm) in .yalm naming (model.cpp:351-377)."""
+    out = {"model.embed.weight": ((c.vocab_size, c.dim), False), "model.norm.weight": ((c.dim,), True)}
+    if not c.tied:
+        out["model.output.weight"] = ((c.vocab_size, c.dim), False)
+    for l in range(c.n_layers):
+        n = layer_names(l)
+        out[n["rms_att"]] = ((c.dim,), True)
+        out[n["rms_ffn"]] = ((c.dim,), True)
+        out[n["wq"]] = ((c.q_dim, c.dim), False)
+        out[n["wk"]] = ((c.kv_dim, c.dim), False)
+        out[n["wv"]] = ((c.kv_dim, c.dim), False)
+        out[n["wo"]] = ((c.dim, c.q_dim), False)
+        out[n["w1"]] = ((c.hidden_dim, c.dim), False)
+        out[n["w2"]] = ((c.dim, c.hidden_dim), False)
+        out[n["w3"]] = ((c.hidden_dim, c.dim), False)
+    return out
+
+
+# ---- deterministic synthetic init (same hash on device and in the oracle) ----
+WEIGHT_SCALE = 0.035  # uniform [-a, a): std 0.02, the usual init scale
+NORM_SCALE, NORM_OFFSET = 0.2, 1.0
+
+
+def synth_seed(base: int, name: str) -> int:
+    """Stable 64-bit seed per tensor name."""
+    h = 1469598103934665603
+    for ch in f"{base}:{name}".encode():
+        h = ((h ^ ch) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def synth_params(name: str, is_norm: bool):
+    return (NORM_SCALE, NORM_OFFSET) if is_norm else (WEIGHT_SCALE, 0.0)
+
+
+def _splitmix64(x):
+    x = (x + np.uint64(0x9E3779B97F4A7C15)).astype(np.uint64)
+    x = ((x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)).astype(np.uint64)
+    x = ((x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)).astype(np.uint64)
+    return x ^ (x >> np.uint64(31))
+
+
+def synth_array(n: int, dtype: int, seed: int, scale: float, offset: float = 0.0) -> np.ndarray:
+    """numpy twin of the device/oracle initialiser (small sizes only)."""
+    with np.errstate(over="ignore"):
+        i = np.arange(n, dtype=np.uint64)
+        h = _splitmix64(np.uint64(seed) ^ (i * np.uint64(0xD1B54A32D192ED03)))
+    s = ((h >> np.uint64(40)).astype(np.int64) - 8388608).astype(np.float32)
+    k = np.float32(scale) * np.float32(1.0 / 8388608.0)
+    if dtype == F32:
+        # fmaf(s, k, offset): exact product (24-bit x 24-bit fits in f64), one rounding
+        return (s.astype(np.float64) * np.float64(k) + np.float64(np.float32(offset))).astype(np.float32)
+    v = (s * k).astype(np.float32)
+    h16 = v.astype(np.float16)
+    if dtype == F16:
+        return h16
+    hb = h16.view(np.uint16).astype(np.uint32)
+    return ((hb + 0x7F + ((hb >> 8) & 1)) >> 8).astype(np.uint8)
+
+
+def synth_host_tensors(c: ModelConfig, seed: int = 1) -> dict:
+    """All tensors of a synthetic model as numpy arrays (norms f32, weights in
+    c.weight_dtype storage: f32 / f16 / uint8 E5M2 bits)."""
+    out = {}
+    for name, (shape, is_norm) in tensor_shapes(c).items():
+        scale, offset = synth_params(name, is_norm)
+        dt = F32 if is_norm else c.weight_dtype
+        n = int(np.prod(shape))
+        out[name] = synth_array(n, dt, synth_seed(seed, name), scale, offset).reshape(shape)
+    return out
+
+
+def e5m2_to_f32(b: np.ndarray) -> np.ndarray:
+    """Exact: the E5M2 byte b is the f16 with bits b << 8."""
+    return (b.astype(np.uint16) << 8).view(np.float16).astype(np.float32)
+
+
+def rope_inv_freq(c: ModelConfig) -> np.ndarray:
+    j = np.arange(0, c.head_dim, 2)
+    with np.errstate(divide="ignore"):
+        f = 1.0 / np.power(np.float32(c.rope_theta), (j / c.rotary_dim).astype(np.float32))
+    f[j >= c.rotary_dim] = 0.0
+    return f.astype(np.float32)
+
+
+def kv_indices(max_seq_len: int, pos: int):
+    """infer.cpp:483-485"""
+    kv_sink = KV_SINKS if pos >= max_seq_len else 0
+    kv_pos = kv_sink + (pos - kv_sink) % (max_seq_len - kv_sink)
+    kv_len = max_seq_len if pos >= max_seq_len else pos + 1
+    return kv_sink, kv_pos, kv_len
+
+
+def nbytes_model(c: ModelConfig) -> int:
+    wb = DTYPE_BYTES[c.weight_dtype]
+    tot = 0
+    for _, (shape, is_norm) in tensor_shapes(c).items():
+        tot += int(np.prod(shape)) * (4 if is_norm else wb)
+    return tot
+

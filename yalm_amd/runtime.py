@@ -1,0 +1,315 @@
+"""ctypes binding of libyalm_hip.so (C ABI: include/yalm_hip.h).
+
+Python mirror of the reference's device-facing API: ``DeviceModel`` is
+``Model::cuda()`` (model.cpp:380-394, weights uploaded once, tied embedding
+not duplicated), ``Decoder`` is ``InferenceState::cuda()`` + ``Model::forward``
+(model.cpp:323-345, 396-407). Every call goes through the HIP library; there
+is no CPU path here (the CPU oracle lives in oracle/, test-only).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from . import models as M
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libyalm_hip.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"{LIB_PATH} is missing: build it with `make -C {os.path.dirname(HERE)}` "
+        "(or __graft_entry__.build()). There is no CPU fallback."
+    )
+
+lib = ctypes.CDLL(LIB_PATH)
+
+c_void_p = ctypes.c_void_p
+c_int = ctypes.c_int
+c_float = ctypes.c_float
+c_size_t = ctypes.c_size_t
+
+
+class Config(ctypes.Structure):
+    """yalm_config (model.h:41-68)."""
+
+    _fields_ = [
+        ("dim", c_int),
+        ("hidden_dim", c_int),
+        ("head_dim", c_int),
+        ("n_layers", c_int),
+        ("n_heads", c_int),
+        ("n_kv_heads", c_int),
+        ("vocab_size", c_int),
+        ("max_seq_len", c_int),
+        ("rope_theta", c_float),
+        ("rotary_dim", c_int),
+        ("norm_eps", c_float),
+        ("act", c_int),
+        ("qkv_clip", c_float),
+        ("weight_dtype", c_int),
+    ]
+
+    @classmethod
+    def from_model(cls, c: M.ModelConfig) -> "Config":
+        return cls(
+            c.dim, c.hidden_dim, c.head_dim, c.n_layers, c.n_heads, c.n_kv_heads, c.vocab_size, c.max_seq_len,
+            c.rope_theta, c.rotary_dim, c.norm_eps, c.act, c.qkv_clip, c.weight_dtype,
+        )
+
+
+class BlockWeights(ctypes.Structure):
+    _fields_ = [(n, c_void_p) for n in ("rms_att", "rms_ffn", "wq", "wk", "wv", "wo", "w1", "w2", "w3",
+                                        "key_cache", "value_cache")]
+
+
+class ModelWeights(ctypes.Structure):
+    _fields_ = [("token_embedding", c_void_p), ("rms_final", c_void_p), ("wcls", c_void_p),
+                ("blocks", ctypes.POINTER(BlockWeights))]
+
+
+def _sig(name, restype, argtypes):
+    f = getattr(lib, name)
+    f.restype = restype
+    f.argtypes = argtypes
+    return f
+
+
+_sig("yalm_last_error", ctypes.c_char_p, [])
+_sig("yalm_set_device", c_int, [c_int])
+_sig("yalm_upload", c_void_p, [c_void_p, c_size_t])
+_sig("yalm_alloc", c_void_p, [c_size_t])
+_sig("yalm_download", c_int, [c_void_p, c_void_p, c_size_t])
+_sig("yalm_register_host", c_int, [c_void_p, c_size_t])
+_sig("yalm_unregister_host", c_int, [c_void_p])
+_sig("yalm_free", c_int, [c_void_p])
+_sig("yalm_stream_create", c_int, [ctypes.POINTER(c_void_p)])
+_sig("yalm_stream_destroy", c_int, [c_void_p])
+_sig("yalm_stream_sync", c_int, [c_void_p])
+_sig("yalm_synth", c_int, [c_void_p, c_size_t, c_int, ctypes.c_uint64, c_float, c_float, c_void_p])
+_sig("yalm_decoder_create", c_int, [ctypes.POINTER(Config), ctypes.POINTER(ModelWeights), c_void_p,
+                                     ctypes.POINTER(c_void_p)])
+_sig("yalm_decoder_destroy", c_int, [c_void_p])
+_sig("yalm_forward", c_int, [c_void_p, c_int, c_int, c_int, c_void_p])
+_sig("yalm_generate_greedy", c_int, [c_void_p, c_int, c_int, c_int, c_void_p])
+_sig("yalm_enqueue_greedy", c_int, [c_void_p, c_int])
+_sig("yalm_device_step", c_int, [c_void_p, ctypes.POINTER(c_int), ctypes.POINTER(c_int)])
+_sig("yalm_block", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int])
+_sig("yalm_get_x", c_int, [c_void_p, c_void_p])
+_sig("yalm_set_x", c_int, [c_void_p, c_void_p])
+_sig("yalm_get_logits", c_int, [c_void_p, c_void_p])
+_sig("yalm_time_kernel", c_int, [c_void_p, c_int, c_int, ctypes.POINTER(c_float)])
+_sig("yalm_kernel_name", ctypes.c_char_p, [c_void_p, c_int])
+_sig("yalm_matmul", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int])
+_sig("yalm_mha", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int])
+_sig("yalm_ffn", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int])
+
+EXPORTED = [
+    "yalm_last_error", "yalm_set_device", "yalm_upload", "yalm_alloc", "yalm_download", "yalm_register_host",
+    "yalm_unregister_host", "yalm_free", "yalm_stream_create", "yalm_stream_destroy", "yalm_stream_sync",
+    "yalm_synth", "yalm_decoder_create", "yalm_decoder_destroy", "yalm_forward", "yalm_generate_greedy",
+    "yalm_enqueue_greedy", "yalm_device_step", "yalm_block", "yalm_get_x", "yalm_set_x", "yalm_get_logits",
+    "yalm_time_kernel", "yalm_kernel_name", "yalm_matmul", "yalm_mha", "yalm_ffn",
+]
+
+HYDRATE_KV_CACHE, OUTPUT_LOGITS = 0, 1
+
+
+class YalmError(RuntimeError):
+    pass
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        raise YalmError(f"yalm error {rc}: {lib.yalm_last_error().decode()}")
+
+
+def _ptr(a: np.ndarray) -> int:
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data
+
+
+# ------------------------------------------------------------- kernel-level test API
+def matmul(x: np.ndarray, w: np.ndarray, dtype: int) -> np.ndarray:
+    """matmul_cuda (infer.cu:937-957): W (d, n) @ x (n,)."""
+    d, n = w.shape
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    w = np.ascontiguousarray(w)
+    out = np.zeros(d, np.float32)
+    check(lib.yalm_matmul(_ptr(out), _ptr(x), _ptr(w), n, d, dtype))
+    return out
+
+
+def mha(kb, vb, q, head_dim, kv_len, max_seq_len, n_heads, n_kv_heads, att_init=None):
+    """mha_cuda (infer.cu:890-935): returns (xout, att)."""
+    kb = np.ascontiguousarray(kb, dtype=np.float16).view(np.uint16)
+    vb = np.ascontiguousarray(vb, dtype=np.float16).view(np.uint16)
+    q = np.ascontiguousarray(q, dtype=np.float32)
+    xout = np.zeros(n_heads * head_dim, np.float32)
+    att = np.zeros(n_heads * max_seq_len, np.float32) if att_init is None else np.array(att_init, np.float32)
+    check(lib.yalm_mha(_ptr(xout), _ptr(att), _ptr(kb), _ptr(vb), _ptr(q), head_dim, kv_len, max_seq_len, n_heads,
+                       n_kv_heads))
+    return xout, att
+
+
+def ffn(x, w1, w2, w3, act: int, dtype: int) -> np.ndarray:
+    """ffn_cuda (infer.cu:959-1007)."""
+    hidden_dim, dim = w1.shape
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    w1, w2, w3 = (np.ascontiguousarray(a) for a in (w1, w2, w3))
+    out = np.zeros(dim, np.float32)
+    check(lib.yalm_ffn(_ptr(out), _ptr(x), _ptr(w1), _ptr(w2), _ptr(w3), hidden_dim, dim, act, dtype))
+    return out
+
+
+# ------------------------------------------------------------- model + decoder
+class DeviceModel:
+    """Model::cuda(): all weights resident in HBM (one allocation per tensor;
+    a tied classifier aliases the embedding instead of a second upload, unlike
+    model.cpp:388/393)."""
+
+    def __init__(self, cfg: M.ModelConfig):
+        self.cfg = cfg
+        self.ptrs: dict = {}
+        self._owned: list = []
+
+    def _alloc(self, nbytes: int) -> int:
+        p = lib.yalm_alloc(nbytes)
+        if not p:
+            raise YalmError(lib.yalm_last_error().decode())
+        self._owned.append(p)
+        return p
+
+    @classmethod
+    def from_arrays(cls, cfg: M.ModelConfig, tensors: dict) -> "DeviceModel":
+        """Upload host tensors (numpy; names as in .yalm)."""
+        self = cls(cfg)
+        for name, (shape, is_norm) in M.tensor_shapes(cfg).items():
+            a = np.ascontiguousarray(tensors[name])
+            p = lib.yalm_upload(a.ctypes.data, a.nbytes)
+            if not p:
+                raise YalmError(lib.yalm_last_error().decode())
+            self._owned.append(p)
+            self.ptrs[name] = p
+        return self
+
+    @classmethod
+    def from_yalm(cls, path: str, context: int = 0) -> "DeviceModel":
+        from .yalmfile import read_yalm
+
+        yd = read_yalm(path)
+        tied = "model.output.weight" not in yd.tensors
+        cfg = M.config_from_metadata(yd.metadata, context, tied)
+        arrays = {k: t.data for k, t in yd.tensors.items()}
+        try:
+            return cls.from_arrays(cfg, arrays)
+        finally:
+            arrays.clear()
+            yd.close()
+
+    @classmethod
+    def synthetic(cls, cfg: M.ModelConfig, seed: int = 1) -> "DeviceModel":
+        """Random-weight model of cfg's shape generated directly in HBM with the
+        deterministic hash shared with the oracle (no PCIe upload)."""
+        self = cls(cfg)
+        for name, (shape, is_norm) in M.tensor_shapes(cfg).items():
+            n = int(np.prod(shape))
+            dt = M.F32 if is_norm else cfg.weight_dtype
+            p = self._alloc(n * M.DTYPE_BYTES[dt])
+            scale, offset = M.synth_params(name, is_norm)
+            check(lib.yalm_synth(p, n, dt, M.synth_seed(seed, name), scale, offset, None))
+            self.ptrs[name] = p
+        check(lib.yalm_stream_sync(None))
+        return self
+
+    def weights_struct(self):
+        cfg = self.cfg
+        blocks = (BlockWeights * cfg.n_layers)()
+        for l in range(cfg.n_layers):
+            n = M.layer_names(l)
+            for k, name in n.items():
+                setattr(blocks[l], k, self.ptrs[name])
+        emb = self.ptrs["model.embed.weight"]
+        wcls = self.ptrs.get("model.output.weight", emb)
+        mw = ModelWeights(emb, self.ptrs["model.norm.weight"], wcls, blocks)
+        return mw, blocks
+
+    def close(self):
+        for p in self._owned:
+            lib.yalm_free(p)
+        self._owned = []
+        self.ptrs = {}
+
+
+class Decoder:
+    """InferenceState on the device + Model::forward (graph-replayed)."""
+
+    def __init__(self, model: DeviceModel):
+        self.model = model
+        self.cfg = model.cfg
+        self._c = Config.from_model(self.cfg)
+        mw, self._blocks = model.weights_struct()
+        self._mw = mw
+        h = c_void_p()
+        check(lib.yalm_decoder_create(ctypes.byref(self._c), ctypes.byref(mw), None, ctypes.byref(h)))
+        self.h = h
+
+    def forward(self, token: int, pos: int, mode: int = OUTPUT_LOGITS):
+        if mode == OUTPUT_LOGITS:
+            out = np.empty(self.cfg.vocab_size, np.float32)
+            check(lib.yalm_forward(self.h, token, pos, mode, out.ctypes.data))
+            return out
+        check(lib.yalm_forward(self.h, token, pos, mode, None))
+        return None
+
+    def generate_greedy(self, token: int, pos: int, n: int) -> list:
+        out = np.zeros(max(n, 1), np.int32)
+        check(lib.yalm_generate_greedy(self.h, token, pos, n, out.ctypes.data))
+        return out[:n].tolist()
+
+    def enqueue_greedy(self, n: int) -> None:
+        check(lib.yalm_enqueue_greedy(self.h, n))
+
+    def device_step(self):
+        t, p = c_int(), c_int()
+        check(lib.yalm_device_step(self.h, ctypes.byref(t), ctypes.byref(p)))
+        return t.value, p.value
+
+    def block(self, layer, pos, kv_sink, kv_pos, kv_len):
+        check(lib.yalm_block(self.h, layer, pos, kv_sink, kv_pos, kv_len))
+
+    def get_x(self) -> np.ndarray:
+        out = np.empty(self.cfg.dim, np.float32)
+        check(lib.yalm_get_x(self.h, out.ctypes.data))
+        return out
+
+    def set_x(self, x: np.ndarray) -> None:
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        check(lib.yalm_set_x(self.h, x.ctypes.data))
+
+    def get_logits(self) -> np.ndarray:
+        out = np.empty(self.cfg.vocab_size, np.float32)
+        check(lib.yalm_get_logits(self.h, out.ctypes.data))
+        return out
+
+    def time_kernel(self, kernel_id: int, iters: int) -> float:
+        ms = c_float()
+        check(lib.yalm_time_kernel(self.h, kernel_id, iters, ctypes.byref(ms)))
+        return ms.value
+
+    def kernel_name(self, kernel_id: int) -> str:
+        return lib.yalm_kernel_name(self.h, kernel_id).decode()
+
+    def close(self):
+        if self.h:
+            check(lib.yalm_decoder_destroy(self.h))
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
