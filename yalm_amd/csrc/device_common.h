@@ -62,6 +62,10 @@ __device__ __forceinline__ float h2f(uint16_t h) {
 	return (float)f;
 }
 __device__ __forceinline__ uint16_t f2h(float x) { // round to nearest even
+	// Opaque barrier: keeps the value's own f32 rounding. Otherwise hipcc fuses a
+	// producing multiply/FMA with the convert (v_fma_mix*_f16, a single rounding),
+	// which differs from the CPU reference's f32-then-f16 (infer.cpp:299, 314).
+	asm volatile("" : "+v"(x));
 	_Float16 f = (_Float16)x;
 	uint16_t h;
 	__builtin_memcpy(&h, &f, 2);
@@ -74,8 +78,12 @@ struct WF32 {
 	static constexpr int BYTES = 4;
 	__device__ static __forceinline__ void unpack(const u32x4_t &w, float *o) {
 #pragma unroll
-		for (int i = 0; i < 4; ++i)
-			o[i] = __builtin_bit_cast(float, w[i]);
+		for (int i = 0; i < 4; ++i) {
+			// copy the element out first: __builtin_bit_cast on a vector-element
+			// lvalue reads element 0 under hipcc 7.2 (found by the GPU parity tests)
+			const uint32_t v = w[i];
+			o[i] = __builtin_bit_cast(float, v);
+		}
 	}
 };
 struct WF16 {
@@ -84,7 +92,8 @@ struct WF16 {
 	__device__ static __forceinline__ void unpack(const u32x4_t &w, float *o) {
 #pragma unroll
 		for (int i = 0; i < 4; ++i) {
-			half2_t h = __builtin_bit_cast(half2_t, w[i]);
+			const uint32_t v = w[i];
+			half2_t h = __builtin_bit_cast(half2_t, v);
 			o[2 * i] = (float)h[0];
 			o[2 * i + 1] = (float)h[1];
 		}

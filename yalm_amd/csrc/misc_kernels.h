@@ -116,7 +116,7 @@ __global__ void synth_kernel(void *dst, size_t n, int dtype, uint64_t seed, floa
 			((float *)dst)[i] = __builtin_fmaf((float)s, k, offset);
 		} else {
 			float v = __fmul_rn((float)s, k);
-			uint32_t hb = f2h(v);
+			uint32_t hb = f2h(v); // f2h keeps the f32 rounding step (no fma_mix fusion)
 			if (dtype == 1)
 				((uint16_t *)dst)[i] = (uint16_t)hb;
 			else
