@@ -7,13 +7,16 @@ CSRC = yalm_amd/csrc
 HIP_SRCS = $(CSRC)/yalm_hip.hip
 HIP_HDRS = $(wildcard $(CSRC)/*.h) include/yalm_hip.h
 
-all: yalm_amd/libyalm_hip.so oracle
+all: yalm_amd/libyalm_hip.so oracle host
 
 yalm_amd/libyalm_hip.so: $(HIP_SRCS) $(HIP_HDRS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(HIP_SRCS)
 
 oracle:
 	$(MAKE) -C oracle
+
+host: yalm_amd/libyalm_hip.so
+	$(MAKE) -C yalm_amd/host
 
 # kernel resource usage (VGPR/SGPR/LDS/occupancy) report
 resource-usage:
@@ -23,5 +26,6 @@ resource-usage:
 clean:
 	rm -f yalm_amd/libyalm_hip.so
 	$(MAKE) -C oracle clean
+	$(MAKE) -C yalm_amd/host clean
 
-.PHONY: all oracle clean resource-usage
+.PHONY: all oracle host clean resource-usage

@@ -137,6 +137,11 @@ int yalm_get_logits(yalm_decoder d, float *host);
  * GEMV, 1 = attention, 2 = Wo GEMV, 3 = W1/W3 GEMV+GLU, 4 = W2 GEMV,
  * 5 = logits GEMV. Used by bench.py for the roofline of the dominant kernel. */
 int yalm_time_kernel(yalm_decoder d, int kernel_id, int iters, float *avg_ms);
+/* Override the GEMV launch geometry of one weight-streaming kernel kind
+ * (0 = QKV, 1 = Wo, 2 = W1/W3, 3 = W2, 4 = logits): workgroup size 256|512,
+ * unroll (chunks in flight per wave) 4|8, row groups per wave; 0 = automatic.
+ * Drops captured graphs (re-captured on next use). Tuning/ablation hook. */
+int yalm_set_gemv_config(yalm_decoder d, int kind, int threads, int unroll, int gpw);
 /* Name of kernel_id's device function (to match rocprofv3 summaries). */
 const char *yalm_kernel_name(yalm_decoder d, int kernel_id);
 

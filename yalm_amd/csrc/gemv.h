@@ -277,3 +277,100 @@ __global__ __launch_bounds__(GEMV_THREADS) void gemv_kernel(P p, const float *__
 		p.finish(g, acc, lane);
 	}
 }
+
+// Streaming GEMV (the production path; requires n % (64 * EPL) == 0).
+//
+// Each wave owns `gpw` consecutive row groups and walks them as ONE flattened
+// stream of 16-byte-per-lane chunks with U chunk-slots of R rows kept in
+// flight: slot u is refilled with chunk k+U right after chunk k is consumed,
+// so the HBM queue never drains at row boundaries. The first U slots are
+// issued before the x staging / rmsnorm prologue so weight latency overlaps
+// it. With the host picking (THREADS, gpw) such that every workgroup of the
+// launch is resident at once (one "wave" of workgroups, choose_gemv_cfg), the
+// per-CU work is balanced to within one row group and there is no tail.
+template <class WT, class P, int U, bool NORM, int THREADS>
+__global__ __launch_bounds__(THREADS) void gemv_stream_kernel(P p, const float *__restrict__ x,
+                                                              const float *__restrict__ normw, float eps, int gpw) {
+	extern __shared__ __attribute__((aligned(16))) float xs[];
+	constexpr int R = P::R;
+	constexpr int EPL = WT::EPL;
+	constexpr int CH = YALM_WAVE * EPL;
+	constexpr size_t CHB = (size_t)CH * WT::BYTES;
+	const int n = p.n;
+	const int nch = n / CH;
+	const int lane = threadIdx.x & 63;
+	const int wave = threadIdx.x >> 6;
+	const int g0 = (blockIdx.x * (THREADS / YALM_WAVE) + wave) * gpw;
+	const int gend = min(g0 + gpw, p.n_groups);
+	const int total = gend > g0 ? (gend - g0) * nch : 0;
+	const size_t lane_off = (size_t)lane * EPL * WT::BYTES;
+
+	int ig = g0, ic = 0; // issue cursor (group, chunk)
+	const char *rp[R];
+#pragma unroll
+	for (int r = 0; r < R; ++r)
+		rp[r] = nullptr;
+	if (total > 0) {
+#pragma unroll
+		for (int r = 0; r < R; ++r)
+			rp[r] = p.row(ig, r) + lane_off;
+	}
+	u32x4_t buf[U][R];
+#pragma unroll
+	for (int u = 0; u < U; ++u) {
+		if (u < total) {
+#pragma unroll
+			for (int r = 0; r < R; ++r)
+				buf[u][r] = load_nt16(rp[r] + ic * CHB);
+			if (++ic == nch) {
+				ic = 0;
+				if (++ig < gend) {
+#pragma unroll
+					for (int r = 0; r < R; ++r)
+						rp[r] = p.row(ig, r) + lane_off;
+				}
+			}
+		}
+	}
+
+	p.prologue();
+	stage_x<NORM>(xs, x, normw, n, eps);
+
+	float acc[R];
+#pragma unroll
+	for (int r = 0; r < R; ++r)
+		acc[r] = 0.0f;
+	int cg = g0, cc = 0; // consume cursor
+	for (int k = 0; k < total; k += U) {
+#pragma unroll
+		for (int u = 0; u < U; ++u) {
+			if (k + u < total) {
+				fma_chunk<WT, R>(acc, buf[u], xs + cc * CH + lane * EPL);
+				if (k + u + U < total) {
+#pragma unroll
+					for (int r = 0; r < R; ++r)
+						buf[u][r] = load_nt16(rp[r] + ic * CHB);
+					if (++ic == nch) {
+						ic = 0;
+						if (++ig < gend) {
+#pragma unroll
+							for (int r = 0; r < R; ++r)
+								rp[r] = p.row(ig, r) + lane_off;
+						}
+					}
+				}
+				if (++cc == nch) {
+#pragma unroll
+					for (int r = 0; r < R; ++r)
+						acc[r] = wave_sum(acc[r]);
+					p.finish(cg, acc, lane);
+#pragma unroll
+					for (int r = 0; r < R; ++r)
+						acc[r] = 0.0f;
+					cc = 0;
+					++cg;
+				}
+			}
+		}
+	}
+}

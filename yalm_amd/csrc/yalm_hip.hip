@@ -136,24 +136,115 @@ extern "C" int yalm_synth(void *device, size_t n, int dtype, uint64_t seed, floa
 }
 
 // ------------------------------------------------------------------ launch helpers
-static int gemv_gpw_default() {
-	return 1;
+// GEMV launch geometry (see gemv_stream_kernel). 0 = automatic.
+struct GemvCfg {
+	int threads = 0, U = 0, gpw = 0;
+};
+enum { GK_QKV = 0, GK_WO = 1, GK_GLU = 2, GK_W2 = 3, GK_CLS = 4, GK_N = 5 };
+
+static int device_cu_count() {
+	static int n = 0;
+	if (!n) {
+		int dev = 0;
+		if (hipGetDevice(&dev) != hipSuccess ||
+		    hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+			n = 256;
+	}
+	return n;
+}
+
+// Default geometry: many small workgroups, one row group per wave, U = 4
+// chunks in flight per row — the hardware dispatcher then balances the CUs
+// dynamically. Measured on MI355X (tools/sweep_gemv.py, profiles/) this beats
+// the "one resident wave of workgroups" geometry of balanced_gemv_cfg by
+// 3-10% on every Mistral-7B GEMV, matching the pure-read streaming envelope
+// of tools/stream_bench.hip (4-16 KB per wave is the sweet spot).
+static GemvCfg default_gemv_cfg(int kind) {
+	if (kind == GK_WO)
+		return GemvCfg{256, 8, 1};
+	if (kind == GK_CLS)
+		return GemvCfg{256, 4, 6};
+	return GemvCfg{512, 4, 1};
+}
+
+// Alternative geometry (tuning hook, threads/gpw = 0 in yalm_set_gemv_config
+// with YALM_GEMV_BALANCED=1): all workgroups resident at once, the busiest CU
+// holding as few row groups as possible, 8..16 waves per CU.
+static GemvCfg balanced_gemv_cfg(int n_groups, size_t lds_bytes, GemvCfg want) {
+	const int ncu = device_cu_count();
+	GemvCfg best;
+	long best_cost = -1;
+	int best_waves = 0;
+	for (int threads : {512, 256}) {
+		if (want.threads && threads != want.threads)
+			continue;
+		const int wpw = threads / YALM_WAVE;
+		const int lds_fit = (int)std::max<size_t>(1, 163840 / std::max<size_t>(lds_bytes, 1));
+		for (int gpw = 1; gpw <= 256; ++gpw) {
+			if (want.gpw && gpw != want.gpw)
+				continue;
+			const long nw = (n_groups + gpw - 1) / gpw;
+			const long nwg = (nw + wpw - 1) / wpw;
+			const long per_cu_wg = (nwg + ncu - 1) / ncu;
+			const long waves_cu = per_cu_wg * wpw;
+			if (per_cu_wg > lds_fit || waves_cu > 16)
+				continue;
+			const long cost = per_cu_wg * wpw * gpw;
+			const bool enough = waves_cu >= 8;
+			const bool best_enough = best_waves >= 8;
+			if (best_cost < 0 || (enough && !best_enough) ||
+			    (enough == best_enough && (cost < best_cost || (cost == best_cost && waves_cu > best_waves)))) {
+				best_cost = cost;
+				best = GemvCfg{threads, 0, gpw};
+				best_waves = (int)waves_cu;
+			}
+		}
+	}
+	if (best_cost < 0)
+		best = GemvCfg{256, 0, std::max(1, (n_groups + ncu * 16 - 1) / (ncu * 16))};
+	best.U = want.U ? want.U : 8;
+	return best;
+}
+
+template <class WT, class P, bool NORM, int THREADS, int U>
+static int launch_stream(const P &p, const float *x, const float *normw, float eps, int gpw, size_t lds,
+                         hipStream_t st) {
+	auto kern = gemv_stream_kernel<WT, P, U, NORM, THREADS>;
+	if (lds > 65536)
+		HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+	const int waves = THREADS / YALM_WAVE;
+	const long nw = (p.n_groups + gpw - 1) / gpw;
+	const int blocks = (int)((nw + waves - 1) / waves);
+	hipLaunchKernelGGL(kern, dim3(blocks), dim3(THREADS), lds, st, p, x, normw, eps, gpw);
+	HIPCHK(hipGetLastError());
+	return YALM_OK;
 }
 
 template <class WT, class P, bool NORM>
-static int launch_gemv(const P &p, const float *x, const float *normw, float eps, int gpw, hipStream_t st) {
-	constexpr int U = 4;
-	const int waves = GEMV_THREADS / YALM_WAVE;
-	const int per_block = waves * gpw;
-	const int blocks = (p.n_groups + per_block - 1) / per_block;
-	const size_t lds = (size_t)((p.n + 3) & ~3) * sizeof(float) + 64;
-	auto kern = gemv_kernel<WT, P, U, NORM>;
-	if (lds > 65536) {
-		HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+static int launch_gemv(const P &p, const float *x, const float *normw, float eps, int kind, GemvCfg want,
+                       hipStream_t st) {
+	const size_t lds = (size_t)((p.n + 3) & ~3) * sizeof(float) + 64 * sizeof(float);
+	constexpr int CH = YALM_WAVE * WT::EPL;
+	if (p.n % CH != 0) { // ragged K: generic kernel (tests / unusual shapes)
+		auto kern = gemv_kernel<WT, P, 4, NORM>;
+		if (lds > 65536)
+			HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+		const int blocks = (p.n_groups + GEMV_THREADS / YALM_WAVE - 1) / (GEMV_THREADS / YALM_WAVE);
+		hipLaunchKernelGGL(kern, dim3(blocks), dim3(GEMV_THREADS), lds, st, p, x, normw, eps, 1);
+		HIPCHK(hipGetLastError());
+		return YALM_OK;
 	}
-	hipLaunchKernelGGL(kern, dim3(blocks), dim3(GEMV_THREADS), lds, st, p, x, normw, eps, gpw);
-	HIPCHK(hipGetLastError());
-	return YALM_OK;
+	static const bool balanced = getenv("YALM_GEMV_BALANCED") && atoi(getenv("YALM_GEMV_BALANCED")) != 0;
+	const GemvCfg def = balanced ? balanced_gemv_cfg(p.n_groups, lds, want) : default_gemv_cfg(kind);
+	GemvCfg c;
+	c.threads = want.threads ? want.threads : def.threads;
+	c.U = want.U ? want.U : def.U;
+	c.gpw = want.gpw ? want.gpw : def.gpw;
+	if (c.threads == 512)
+		return c.U == 4 ? launch_stream<WT, P, NORM, 512, 4>(p, x, normw, eps, c.gpw, lds, st)
+		                : launch_stream<WT, P, NORM, 512, 8>(p, x, normw, eps, c.gpw, lds, st);
+	return c.U == 4 ? launch_stream<WT, P, NORM, 256, 4>(p, x, normw, eps, c.gpw, lds, st)
+	                : launch_stream<WT, P, NORM, 256, 8>(p, x, normw, eps, c.gpw, lds, st);
 }
 
 static bool attn_supported(int head_dim, int G) {
@@ -163,43 +254,48 @@ static bool attn_supported(int head_dim, int G) {
 
 template <int D>
 static void launch_attn_D(int G, const float *q, const uint16_t *kc, const uint16_t *vc, const StepState *step,
-                          int n_heads, int n_kv, int max_seq_len, int chunk, int nsplit, float *part, float *att,
-                          float *out, hipStream_t st) {
+                          int n_heads, int n_kv, int max_seq_len, int nsplit, float *part, unsigned *counters,
+                          float *att, float *out, hipStream_t st) {
 	dim3 grid(n_kv, nsplit);
+#define YALM_ATTN(GT)                                                                                                  \
+	attn_decode_kernel<D, GT><<<grid, ATTN_THREADS, 0, st>>>(q, kc, vc, step, n_heads, n_kv, max_seq_len, nsplit,    \
+	                                                         part, counters, out, att)
 	if (G <= 1)
-		attn_split_kernel<D, 1><<<grid, ATTN_THREADS, 0, st>>>(q, kc, vc, step, n_heads, n_kv, max_seq_len, chunk,
-		                                                       nsplit, part, att);
+		YALM_ATTN(1);
 	else if (G <= 2)
-		attn_split_kernel<D, 2><<<grid, ATTN_THREADS, 0, st>>>(q, kc, vc, step, n_heads, n_kv, max_seq_len, chunk,
-		                                                       nsplit, part, att);
+		YALM_ATTN(2);
 	else if (G <= 4)
-		attn_split_kernel<D, 4><<<grid, ATTN_THREADS, 0, st>>>(q, kc, vc, step, n_heads, n_kv, max_seq_len, chunk,
-		                                                       nsplit, part, att);
+		YALM_ATTN(4);
 	else
-		attn_split_kernel<D, 8><<<grid, ATTN_THREADS, 0, st>>>(q, kc, vc, step, n_heads, n_kv, max_seq_len, chunk,
-		                                                       nsplit, part, att);
-	attn_combine_kernel<D><<<n_heads, 128, 0, st>>>(part, step, chunk, nsplit, max_seq_len, out, att);
+		YALM_ATTN(8);
+#undef YALM_ATTN
 }
 
+static int attn_nsplit(int max_seq_len) {
+	return (max_seq_len + ATTN_CHUNK - 1) / ATTN_CHUNK;
+}
+
+// part: (n_heads, nsplit, head_dim + 2) floats; counters: n_kv zeroed words.
 static int launch_attn(int head_dim, int n_heads, int n_kv, const float *q, const uint16_t *kc, const uint16_t *vc,
-                       const StepState *step, int max_seq_len, int chunk, int nsplit, float *part, float *att,
+                       const StepState *step, int max_seq_len, float *part, unsigned *counters, float *att,
                        float *out, hipStream_t st) {
 	const int G = n_heads / n_kv;
+	const int nsplit = attn_nsplit(max_seq_len);
 	switch (head_dim) {
 	case 16:
-		launch_attn_D<16>(G, q, kc, vc, step, n_heads, n_kv, max_seq_len, chunk, nsplit, part, att, out, st);
+		launch_attn_D<16>(G, q, kc, vc, step, n_heads, n_kv, max_seq_len, nsplit, part, counters, att, out, st);
 		break;
 	case 32:
-		launch_attn_D<32>(G, q, kc, vc, step, n_heads, n_kv, max_seq_len, chunk, nsplit, part, att, out, st);
+		launch_attn_D<32>(G, q, kc, vc, step, n_heads, n_kv, max_seq_len, nsplit, part, counters, att, out, st);
 		break;
 	case 64:
-		launch_attn_D<64>(G, q, kc, vc, step, n_heads, n_kv, max_seq_len, chunk, nsplit, part, att, out, st);
+		launch_attn_D<64>(G, q, kc, vc, step, n_heads, n_kv, max_seq_len, nsplit, part, counters, att, out, st);
 		break;
 	case 128:
-		launch_attn_D<128>(G, q, kc, vc, step, n_heads, n_kv, max_seq_len, chunk, nsplit, part, att, out, st);
+		launch_attn_D<128>(G, q, kc, vc, step, n_heads, n_kv, max_seq_len, nsplit, part, counters, att, out, st);
 		break;
 	case 256:
-		launch_attn_D<256>(G, q, kc, vc, step, n_heads, n_kv, max_seq_len, chunk, nsplit, part, att, out, st);
+		launch_attn_D<256>(G, q, kc, vc, step, n_heads, n_kv, max_seq_len, nsplit, part, counters, att, out, st);
 		break;
 	default:
 		set_err("unsupported head_dim");
@@ -207,16 +303,6 @@ static int launch_attn(int head_dim, int n_heads, int n_kv, const float *q, cons
 	}
 	HIPCHK(hipGetLastError());
 	return YALM_OK;
-}
-
-static int attn_chunk_default() {
-	const char *e = getenv("YALM_ATTN_CHUNK");
-	int c = e ? atoi(e) : 128;
-	if (c < 16)
-		c = 16;
-	if (c > ATTN_MAXCHUNK)
-		c = ATTN_MAXCHUNK;
-	return c;
 }
 
 // ------------------------------------------------------------------ decoder
@@ -239,8 +325,10 @@ struct yalm_decoder_s {
 	std::vector<void *> dev_allocs;
 	hipGraph_t graph[N_GRAPHS] = {};
 	hipGraphExec_t exec[N_GRAPHS] = {};
-	int chunk = 128, nsplit = 1;
-	int gpw = 1;
+	unsigned *attn_counters = nullptr; // per-kv-head arrival tickets (zeroed; the last arriver resets)
+	GemvCfg gemv[GK_N];
+	bool eager = false;     // YALM_EAGER=1: launch kernels directly (profilers that mis-handle graph replay)
+	bool graph_sync = false; // YALM_GRAPH_SYNC=1: synchronise after every replay
 	std::string kname;
 };
 
@@ -266,17 +354,17 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 		p.q_out = d->q;
 		p.kcache = w.key_cache;
 		p.vcache = w.value_cache;
-		TRY((launch_gemv<WT, PQKV<WT>, true>(p, d->x, w.rms_att, c.norm_eps, d->gpw, st)));
+		TRY((launch_gemv<WT, PQKV<WT>, true>(p, d->x, w.rms_att, c.norm_eps, GK_QKV, d->gemv[GK_QKV], st)));
 	}
 	TRY(launch_attn(c.head_dim, c.n_heads, c.n_kv_heads, d->q, w.key_cache, w.value_cache, d->step, c.max_seq_len,
-	                d->chunk, d->nsplit, d->part, nullptr, d->xb2, st));
+	                d->part, d->attn_counters, nullptr, d->xb2, st));
 	{
 		PResidual<WT, 1> p;
 		p.W = (const char *)w.wo;
 		p.n = q_dim;
 		p.out = d->x;
 		p.n_groups = c.dim;
-		TRY((launch_gemv<WT, PResidual<WT, 1>, false>(p, d->xb2, nullptr, 0.f, d->gpw, st)));
+		TRY((launch_gemv<WT, PResidual<WT, 1>, false>(p, d->xb2, nullptr, 0.f, GK_WO, d->gemv[GK_WO], st)));
 	}
 	if (c.act == YALM_SILU) {
 		PGlu<WT, 1> p;
@@ -285,7 +373,7 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 		p.n = c.dim;
 		p.out = d->hb;
 		p.n_groups = c.hidden_dim;
-		TRY((launch_gemv<WT, PGlu<WT, 1>, true>(p, d->x, w.rms_ffn, c.norm_eps, d->gpw, st)));
+		TRY((launch_gemv<WT, PGlu<WT, 1>, true>(p, d->x, w.rms_ffn, c.norm_eps, GK_GLU, d->gemv[GK_GLU], st)));
 	} else {
 		PGlu<WT, 0> p;
 		p.w1 = (const char *)w.w1;
@@ -293,7 +381,7 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 		p.n = c.dim;
 		p.out = d->hb;
 		p.n_groups = c.hidden_dim;
-		TRY((launch_gemv<WT, PGlu<WT, 0>, true>(p, d->x, w.rms_ffn, c.norm_eps, d->gpw, st)));
+		TRY((launch_gemv<WT, PGlu<WT, 0>, true>(p, d->x, w.rms_ffn, c.norm_eps, GK_GLU, d->gemv[GK_GLU], st)));
 	}
 	{
 		PResidual<WT, 1> p;
@@ -301,7 +389,7 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 		p.n = c.hidden_dim;
 		p.out = d->x;
 		p.n_groups = c.dim;
-		TRY((launch_gemv<WT, PResidual<WT, 1>, false>(p, d->hb, nullptr, 0.f, d->gpw, st)));
+		TRY((launch_gemv<WT, PResidual<WT, 1>, false>(p, d->hb, nullptr, 0.f, GK_W2, d->gemv[GK_W2], st)));
 	}
 	return YALM_OK;
 }
@@ -315,14 +403,14 @@ static int enqueue_logits_t(yalm_decoder_s *d) {
 		p.n = c.dim;
 		p.out = d->logits;
 		p.n_groups = c.vocab_size / 2;
-		return launch_gemv<WT, PStore<WT, 2>, true>(p, d->x, d->rms_final, c.norm_eps, d->gpw, d->stream);
+		return launch_gemv<WT, PStore<WT, 2>, true>(p, d->x, d->rms_final, c.norm_eps, GK_CLS, d->gemv[GK_CLS], d->stream);
 	}
 	PStore<WT, 1> p;
 	p.W = (const char *)d->wcls;
 	p.n = c.dim;
 	p.out = d->logits;
 	p.n_groups = c.vocab_size;
-	return launch_gemv<WT, PStore<WT, 1>, true>(p, d->x, d->rms_final, c.norm_eps, d->gpw, d->stream);
+	return launch_gemv<WT, PStore<WT, 1>, true>(p, d->x, d->rms_final, c.norm_eps, GK_CLS, d->gemv[GK_CLS], d->stream);
 }
 
 template <class WT>
@@ -355,7 +443,7 @@ static int enqueue_forward(yalm_decoder_s *d, int which) {
 }
 
 static int ensure_graph(yalm_decoder_s *d, int which) {
-	if (d->exec[which])
+	if (d->exec[which] || d->eager)
 		return YALM_OK;
 	HIPCHK(hipStreamBeginCapture(d->stream, hipStreamCaptureModeRelaxed));
 	int r = enqueue_forward(d, which);
@@ -409,6 +497,17 @@ static int dalloc(yalm_decoder_s *d, void **p, size_t bytes) {
 	return YALM_OK;
 }
 
+// One forward of graph `which`: a graph replay, or the same kernels launched
+// eagerly when d->eager.
+static int replay(yalm_decoder_s *d, int which) {
+	if (d->eager)
+		return enqueue_forward(d, which);
+	HIPCHK(hipGraphLaunch(d->exec[which], d->stream));
+	if (d->graph_sync)
+		HIPCHK(hipStreamSynchronize(d->stream));
+	return YALM_OK;
+}
+
 extern "C" int yalm_decoder_create(const yalm_config *config, const yalm_model_weights *weights, yalm_stream s,
                                    yalm_decoder *out) {
 	ARGCHK(config && weights && out && weights->blocks, "yalm_decoder_create: null argument");
@@ -435,18 +534,16 @@ extern "C" int yalm_decoder_create(const yalm_config *config, const yalm_model_w
 	}
 	const yalm_config &c = d->c;
 	const int q_dim = c.n_heads * c.head_dim, kv_dim = c.n_kv_heads * c.head_dim;
-	d->chunk = attn_chunk_default();
-	d->nsplit = (c.max_seq_len + d->chunk - 1) / d->chunk;
+	const int nsplit = attn_nsplit(c.max_seq_len);
 	d->tokens_cap = 1 << 16;
-	const char *g = getenv("YALM_GEMV_GPW");
-	d->gpw = g ? atoi(g) : gemv_gpw_default();
-	if (d->gpw < 1)
-		d->gpw = 1;
+	d->eager = getenv("YALM_EAGER") && atoi(getenv("YALM_EAGER")) != 0;
+	d->graph_sync = getenv("YALM_GRAPH_SYNC") && atoi(getenv("YALM_GRAPH_SYNC")) != 0;
 	if ((r = dalloc(d, (void **)&d->step, sizeof(StepState))) || (r = dalloc(d, (void **)&d->x, sizeof(float) * c.dim)) ||
 	    (r = dalloc(d, (void **)&d->q, sizeof(float) * q_dim)) ||
 	    (r = dalloc(d, (void **)&d->xb2, sizeof(float) * q_dim)) ||
 	    (r = dalloc(d, (void **)&d->hb, sizeof(float) * c.hidden_dim)) ||
-	    (r = dalloc(d, (void **)&d->part, sizeof(float) * (size_t)c.n_heads * d->nsplit * (c.head_dim + 2))) ||
+	    (r = dalloc(d, (void **)&d->part, sizeof(float) * (size_t)c.n_heads * nsplit * (c.head_dim + 2))) ||
+	    (r = dalloc(d, (void **)&d->attn_counters, sizeof(unsigned) * c.n_kv_heads)) ||
 	    (r = dalloc(d, (void **)&d->logits, sizeof(float) * c.vocab_size)) ||
 	    (r = dalloc(d, (void **)&d->inv_freq, sizeof(float) * c.head_dim / 2)) ||
 	    (r = dalloc(d, (void **)&d->tokens, sizeof(int) * d->tokens_cap)))
@@ -495,7 +592,7 @@ extern "C" int yalm_forward(yalm_decoder d, int token, int pos, int mode, float 
 	TRY(ensure_graph(d, which));
 	set_step_kernel<<<1, 1, 0, d->stream>>>(d->step, token, pos, 0);
 	HIPCHK(hipGetLastError());
-	HIPCHK(hipGraphLaunch(d->exec[which], d->stream));
+	TRY(replay(d, which));
 	if (which == GRAPH_LOGITS) {
 		HIPCHK(hipStreamSynchronize(d->stream));
 		if (logits_host)
@@ -508,7 +605,7 @@ extern "C" int yalm_enqueue_greedy(yalm_decoder d, int n_steps) {
 	ARGCHK(d, "null decoder");
 	TRY(ensure_graph(d, GRAPH_GREEDY));
 	for (int i = 0; i < n_steps; ++i)
-		HIPCHK(hipGraphLaunch(d->exec[GRAPH_GREEDY], d->stream));
+		TRY(replay(d, GRAPH_GREEDY));
 	return YALM_OK;
 }
 
@@ -527,7 +624,7 @@ extern "C" int yalm_generate_greedy(yalm_decoder d, int token, int pos, int n_st
 		HIPCHK(hipGetLastError());
 		first = false;
 		for (int i = 0; i < batch; ++i)
-			HIPCHK(hipGraphLaunch(d->exec[GRAPH_GREEDY], d->stream));
+			TRY(replay(d, GRAPH_GREEDY));
 		HIPCHK(hipMemcpyAsync(out_tokens + done, d->tokens, sizeof(int) * batch, hipMemcpyDeviceToHost, d->stream));
 		HIPCHK(hipStreamSynchronize(d->stream));
 		done += batch;
@@ -606,7 +703,7 @@ static int enqueue_one_t(yalm_decoder_s *d, int kernel_id, int l) {
 			p.q_out = d->q;
 			p.kcache = w.key_cache;
 			p.vcache = w.value_cache;
-			return launch_gemv<WT, PQKV<WT>, true>(p, d->x, w.rms_att, c.norm_eps, d->gpw, d->stream);
+			return launch_gemv<WT, PQKV<WT>, true>(p, d->x, w.rms_att, c.norm_eps, GK_QKV, d->gemv[GK_QKV], d->stream);
 		}
 		if (kernel_id == 2 || kernel_id == 4) {
 			PResidual<WT, 1> p;
@@ -614,7 +711,7 @@ static int enqueue_one_t(yalm_decoder_s *d, int kernel_id, int l) {
 			p.n = kernel_id == 2 ? q_dim : c.hidden_dim;
 			p.out = d->x;
 			p.n_groups = c.dim;
-			return launch_gemv<WT, PResidual<WT, 1>, false>(p, kernel_id == 2 ? d->xb2 : d->hb, nullptr, 0.f, d->gpw,
+			return launch_gemv<WT, PResidual<WT, 1>, false>(p, kernel_id == 2 ? d->xb2 : d->hb, nullptr, 0.f, kernel_id == 2 ? GK_WO : GK_W2, d->gemv[kernel_id == 2 ? GK_WO : GK_W2],
 			                                               d->stream);
 		}
 		PGlu<WT, 1> p;
@@ -623,11 +720,11 @@ static int enqueue_one_t(yalm_decoder_s *d, int kernel_id, int l) {
 		p.n = c.dim;
 		p.out = d->hb;
 		p.n_groups = c.hidden_dim;
-		return launch_gemv<WT, PGlu<WT, 1>, true>(p, d->x, w.rms_ffn, c.norm_eps, d->gpw, d->stream);
+		return launch_gemv<WT, PGlu<WT, 1>, true>(p, d->x, w.rms_ffn, c.norm_eps, GK_GLU, d->gemv[GK_GLU], d->stream);
 	}
 	case 1:
 		return launch_attn(c.head_dim, c.n_heads, c.n_kv_heads, d->q, w.key_cache, w.value_cache, d->step,
-		                   c.max_seq_len, d->chunk, d->nsplit, d->part, nullptr, d->xb2, d->stream);
+		                   c.max_seq_len, d->part, d->attn_counters, nullptr, d->xb2, d->stream);
 	case 5:
 		return enqueue_logits_t<WT>(d);
 	}
@@ -656,6 +753,25 @@ extern "C" int yalm_time_kernel(yalm_decoder d, int kernel_id, int iters, float 
 	return YALM_OK;
 }
 
+extern "C" int yalm_set_gemv_config(yalm_decoder d, int kind, int threads, int unroll, int gpw) {
+	ARGCHK(d && kind >= 0 && kind < GK_N, "bad decoder/kind");
+	ARGCHK(threads == 0 || threads == 256 || threads == 512, "threads must be 0, 256 or 512");
+	ARGCHK(unroll == 0 || unroll == 4 || unroll == 8, "unroll must be 0, 4 or 8");
+	ARGCHK(gpw >= 0, "gpw must be >= 0");
+	d->gemv[kind] = GemvCfg{threads, unroll, gpw};
+	// captured graphs bake the old geometry: drop them
+	HIPCHK(hipStreamSynchronize(d->stream));
+	for (int i = 0; i < N_GRAPHS; ++i) {
+		if (d->exec[i])
+			(void)hipGraphExecDestroy(d->exec[i]);
+		if (d->graph[i])
+			(void)hipGraphDestroy(d->graph[i]);
+		d->exec[i] = nullptr;
+		d->graph[i] = nullptr;
+	}
+	return YALM_OK;
+}
+
 extern "C" const char *yalm_kernel_name(yalm_decoder d, int kernel_id) {
 	if (!d)
 		return "";
@@ -663,20 +779,20 @@ extern "C" const char *yalm_kernel_name(yalm_decoder d, int kernel_id) {
 	std::string s;
 	switch (kernel_id) {
 	case 0:
-		s = std::string("gemv_kernel<") + wt + ", PQKV<";
+		s = std::string("gemv_stream_kernel<") + wt + ", PQKV<";
 		break;
 	case 1:
-		s = "attn_split_kernel<";
+		s = "attn_decode_kernel<";
 		break;
 	case 2:
 	case 4:
-		s = std::string("gemv_kernel<") + wt + ", PResidual<";
+		s = std::string("gemv_stream_kernel<") + wt + ", PResidual<";
 		break;
 	case 3:
-		s = std::string("gemv_kernel<") + wt + ", PGlu<";
+		s = std::string("gemv_stream_kernel<") + wt + ", PGlu<";
 		break;
 	case 5:
-		s = std::string("gemv_kernel<") + wt + ", PStore<";
+		s = std::string("gemv_stream_kernel<") + wt + ", PStore<";
 		break;
 	default:
 		s = "";
@@ -714,7 +830,7 @@ static int matmul_t(float *out, const float *x, const void *w, int n, int d) {
 	p.n = n;
 	p.out = out;
 	p.n_groups = d;
-	return launch_gemv<WT, PStore<WT, 1>, false>(p, x, nullptr, 0.f, 1, nullptr);
+	return launch_gemv<WT, PStore<WT, 1>, false>(p, x, nullptr, 0.f, GK_GLU, GemvCfg{}, nullptr);
 }
 
 extern "C" int yalm_matmul(float *xout, const float *x, const void *w, int n, int d, int dtype) {
@@ -740,9 +856,8 @@ extern "C" int yalm_mha(float *xout, float *att, const uint16_t *kb, const uint1
 		return YALM_ERR_UNSUPPORTED;
 	}
 	const size_t kvn = (size_t)max_seq_len * n_kv_heads * head_dim;
-	const int chunk = attn_chunk_default();
-	const int nsplit = (max_seq_len + chunk - 1) / chunk;
-	DevBuf dk, dv, dq, dout, datt, dpart, dstep;
+	const int nsplit = attn_nsplit(max_seq_len);
+	DevBuf dk, dv, dq, dout, datt, dpart, dstep, dcnt;
 	TRY(up(dk, kb, kvn * 2));
 	TRY(up(dv, vb, kvn * 2));
 	TRY(up(dq, q, sizeof(float) * n_heads * head_dim));
@@ -750,10 +865,11 @@ extern "C" int yalm_mha(float *xout, float *att, const uint16_t *kb, const uint1
 	TRY(up(datt, att, sizeof(float) * (size_t)n_heads * max_seq_len));
 	TRY(up(dpart, nullptr, sizeof(float) * (size_t)n_heads * nsplit * (head_dim + 2)));
 	TRY(up(dstep, nullptr, sizeof(StepState)));
+	TRY(up(dcnt, nullptr, sizeof(unsigned) * n_kv_heads));
 	set_step_full_kernel<<<1, 1>>>((StepState *)dstep.p, kv_len - 1, 0, kv_len - 1, kv_len);
 	TRY(launch_attn(head_dim, n_heads, n_kv_heads, (const float *)dq.p, (const uint16_t *)dk.p,
-	                (const uint16_t *)dv.p, (const StepState *)dstep.p, max_seq_len, chunk, nsplit,
-	                (float *)dpart.p, att ? (float *)datt.p : nullptr, (float *)dout.p, nullptr));
+	                (const uint16_t *)dv.p, (const StepState *)dstep.p, max_seq_len, (float *)dpart.p,
+	                (unsigned *)dcnt.p, att ? (float *)datt.p : nullptr, (float *)dout.p, nullptr));
 	HIPCHK(hipDeviceSynchronize());
 	HIPCHK(hipMemcpy(xout, dout.p, sizeof(float) * n_heads * head_dim, hipMemcpyDeviceToHost));
 	if (att)
@@ -771,7 +887,7 @@ static int ffn_t(float *out, const float *x, const void *w1, const void *w2, con
 		p.n = dim;
 		p.out = hb;
 		p.n_groups = hidden;
-		TRY((launch_gemv<WT, PGlu<WT, 1>, false>(p, x, nullptr, 0.f, 1, nullptr)));
+		TRY((launch_gemv<WT, PGlu<WT, 1>, false>(p, x, nullptr, 0.f, GK_GLU, GemvCfg{}, nullptr)));
 	} else {
 		PGlu<WT, 0> p;
 		p.w1 = (const char *)w1;
@@ -779,14 +895,14 @@ static int ffn_t(float *out, const float *x, const void *w1, const void *w2, con
 		p.n = dim;
 		p.out = hb;
 		p.n_groups = hidden;
-		TRY((launch_gemv<WT, PGlu<WT, 0>, false>(p, x, nullptr, 0.f, 1, nullptr)));
+		TRY((launch_gemv<WT, PGlu<WT, 0>, false>(p, x, nullptr, 0.f, GK_GLU, GemvCfg{}, nullptr)));
 	}
 	PStore<WT, 1> p;
 	p.W = (const char *)w2;
 	p.n = hidden;
 	p.out = out;
 	p.n_groups = dim;
-	return launch_gemv<WT, PStore<WT, 1>, false>(p, hb, nullptr, 0.f, 1, nullptr);
+	return launch_gemv<WT, PStore<WT, 1>, false>(p, hb, nullptr, 0.f, GK_GLU, GemvCfg{}, nullptr);
 }
 
 extern "C" int yalm_ffn(float *xout, const float *x, const void *w1, const void *w2, const void *w3, int hidden_dim,

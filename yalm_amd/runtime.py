@@ -103,6 +103,7 @@ _sig("yalm_set_x", c_int, [c_void_p, c_void_p])
 _sig("yalm_get_logits", c_int, [c_void_p, c_void_p])
 _sig("yalm_time_kernel", c_int, [c_void_p, c_int, c_int, ctypes.POINTER(c_float)])
 _sig("yalm_kernel_name", ctypes.c_char_p, [c_void_p, c_int])
+_sig("yalm_set_gemv_config", c_int, [c_void_p, c_int, c_int, c_int, c_int])
 _sig("yalm_matmul", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int])
 _sig("yalm_mha", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int])
 _sig("yalm_ffn", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int])
@@ -112,7 +113,7 @@ EXPORTED = [
     "yalm_unregister_host", "yalm_free", "yalm_stream_create", "yalm_stream_destroy", "yalm_stream_sync",
     "yalm_synth", "yalm_decoder_create", "yalm_decoder_destroy", "yalm_forward", "yalm_generate_greedy",
     "yalm_enqueue_greedy", "yalm_device_step", "yalm_block", "yalm_get_x", "yalm_set_x", "yalm_get_logits",
-    "yalm_time_kernel", "yalm_kernel_name", "yalm_matmul", "yalm_mha", "yalm_ffn",
+    "yalm_time_kernel", "yalm_kernel_name", "yalm_set_gemv_config", "yalm_matmul", "yalm_mha", "yalm_ffn",
 ]
 
 HYDRATE_KV_CACHE, OUTPUT_LOGITS = 0, 1
@@ -299,6 +300,9 @@ class Decoder:
         ms = c_float()
         check(lib.yalm_time_kernel(self.h, kernel_id, iters, ctypes.byref(ms)))
         return ms.value
+
+    def set_gemv_config(self, kind: int, threads: int = 0, unroll: int = 0, gpw: int = 0) -> None:
+        check(lib.yalm_set_gemv_config(self.h, kind, threads, unroll, gpw))
 
     def kernel_name(self, kernel_id: int) -> str:
         return lib.yalm_kernel_name(self.h, kernel_id).decode()
