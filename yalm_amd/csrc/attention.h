@@ -2,17 +2,26 @@
 // token over the fp16 sliding-window KV cache, wave64-native, one launch.
 //
 // Replaces attn_dot / attn_softmax / att_mix (infer.cu:338-524: three launches,
-// 32-lane layout, each K/V row re-read once per query head). Here one
-// workgroup owns (kv head g, key chunk s): every K and V row of the chunk is
-// read from HBM exactly once — K and V loads are issued together up front —
-// and serves all G = n_heads / n_kv_heads query heads of the group.
-// Semantics follow the CPU oracle attn (infer.cpp:216-248):
-//   s_t = (q . k_t) / sqrt(head_dim);  p = softmax(s);  out = sum_t p_t v_t.
-// Chunks are merged inside the same launch: each workgroup publishes its
-// (max, sum, unnormalised out) partial, takes an arrival ticket, and the last
-// workgroup of kv head g combines all chunks in chunk order (deterministic,
-// independent of arrival order) — the agent-scope release/acquire hand-off of
-// cdna_hip_programming.md Guideline 16 / "In-launch split-K reduction".
+// 32-lane layout, each K/V row re-read once per query head). One workgroup
+// (4 waves) owns (kv head g, key chunk s of CHUNK rows): every K and V row of
+// the chunk is read from HBM exactly once and serves all G = n_heads /
+// n_kv_heads query heads of the group. Semantics follow the CPU oracle attn
+// (infer.cpp:216-248):  s_t = (q . k_t) / sqrt(head_dim);  p = softmax(s);
+// out = sum_t p_t v_t.
+//
+// Decode attention is latency-bound, so the kernel is built around round
+// trips: K/V rows are read as 16-byte pieces (D/8 lanes per row); the
+// cross-lane sums go through LDS (shuffles lower to serialised ds_bpermute
+// round trips on gfx950) and the softmax reductions use DPP; chunks are
+// small (64 keys) so the KV read spreads over many CUs, and all K, V and q
+// loads are issued speculatively before kv_len is known (rows past kv_len are
+// read but masked), overlapping the step-state load.
+//  * kv_len <= CHUNK: the workgroup normalises and writes the heads directly.
+//    Longer contexts publish (max, sum, unnormalised out) per chunk with
+//    write-through (sc1) stores and an agent-scope arrival ticket; the last
+//    workgroup of kv head g merges all chunks in chunk order (deterministic)
+//    with sc1 loads — the fence-free hand-off of MI355X_MICROARCH.md
+//    §visibility "Valid forms", row 1.
 #pragma once
 
 #include <float.h>
@@ -21,7 +30,21 @@
 
 #define ATTN_THREADS 256
 #define ATTN_WAVES (ATTN_THREADS / YALM_WAVE)
-#define ATTN_CHUNK 128
+
+// Keys per workgroup. Small on purpose: one CU streams only ~50-100 GB/s, so
+// a decode-size KV read must be spread over many CUs to be fast (kv 4096 ->
+// 64 chunks x n_kv_heads workgroups); the merge is a cheap sc1 hand-off.
+template <int D>
+constexpr int attn_chunk() {
+	return 64;
+}
+
+__device__ __forceinline__ void st_sc1(float *p, float v) {
+	__hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float *p) {
+	return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // D = head_dim (multiple of 8, D/8 a power of two <= 64); GT >= G.
 template <int D, int GT>
@@ -29,79 +52,93 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_decode_kernel(
     const float *__restrict__ q, const uint16_t *__restrict__ kc, const uint16_t *__restrict__ vc,
     const StepState *__restrict__ step, int n_heads, int n_kv_heads, int max_seq_len, int nsplit,
     float *__restrict__ part, unsigned *__restrict__ counters, float *__restrict__ out, float *__restrict__ att_dbg) {
-	constexpr int LPK = D / 8;                       // lanes per K/V row, 16 B each
-	constexpr int KPW = 64 / LPK;                    // rows per wave-instruction
-	constexpr int RSTEP = ATTN_WAVES * KPW;          // rows per workgroup-instruction
-	constexpr int NK = (ATTN_CHUNK + RSTEP - 1) / RSTEP; // rows per lane
-	__shared__ float sc[GT][ATTN_CHUNK];
-	__shared__ float red[ATTN_WAVES][GT][D];
+	constexpr int CHUNK = attn_chunk<D>();
+	constexpr int LPK = D / 8;                     // lanes per K/V row, 16 B each
+	constexpr int KPW = 64 / LPK;                  // rows per wave-instruction
+	constexpr int RSTEP = ATTN_WAVES * KPW;        // rows per workgroup-instruction
+	constexpr int NK = (CHUNK + RSTEP - 1) / RSTEP; // rows per lane
+	__shared__ __attribute__((aligned(16))) float sp[GT * CHUNK * LPK]; // per-lane partial dots
+	__shared__ float sc[GT][CHUNK];
+	__shared__ __attribute__((aligned(16))) float red[ATTN_WAVES * KPW][GT][D]; // per-row-slot P.V partials
 	__shared__ float ml[GT][2];
 	__shared__ int last_flag;
 
 	const int g = blockIdx.x;
 	const int s = blockIdx.y;
-	const int kv_len = step->kv_len;
-	const int t0 = s * ATTN_CHUNK;
-	if (t0 >= kv_len)
-		return; // whole workgroup exits before any barrier
-	const int nt = min(ATTN_CHUNK, kv_len - t0);
-	const int ns = (kv_len + ATTN_CHUNK - 1) / ATTN_CHUNK;
+	const int t0 = s * CHUNK;
 	const int G = n_heads / n_kv_heads;
 	const int kv_dim = n_kv_heads * D;
 	const int lane = threadIdx.x & 63;
 	const int wave = threadIdx.x >> 6;
+	const int tid = threadIdx.x;
 	const int sub = lane / LPK;
 	const int piece = lane % LPK;
 	const int tl0 = wave * KPW + sub;
 
-	// issue every K and V load of this lane first (one HBM round trip)
-	// (rows past the chunk end re-load the last valid row: unconditional loads
-	// keep hipcc from branching around each one with a vmcnt(0) wait)
+	// ---- speculative loads (chunk rows clamped to the cache, q, step) in flight together
 	u32x4_t kw[NK], vw[NK];
 #pragma unroll
 	for (int i = 0; i < NK; ++i) {
-		const int tl = min(tl0 + i * RSTEP, nt - 1);
-		const size_t off = (size_t)(t0 + tl) * kv_dim + g * D + piece * 8;
+		const int t = min(t0 + tl0 + i * RSTEP, max_seq_len - 1);
+		const size_t off = (size_t)t * kv_dim + g * D + piece * 8;
 		kw[i] = load16(kc + off);
 		vw[i] = load16(vc + off);
 	}
 	float qr[GT][8];
 #pragma unroll
 	for (int h = 0; h < GT; ++h) {
-		if (h < G) {
-			const float *qp = q + (size_t)(g * G + h) * D + piece * 8;
-			float4_t a = *(const float4_t *)qp;
-			float4_t b = *(const float4_t *)(qp + 4);
-			qr[h][0] = a[0], qr[h][1] = a[1], qr[h][2] = a[2], qr[h][3] = a[3];
-			qr[h][4] = b[0], qr[h][5] = b[1], qr[h][6] = b[2], qr[h][7] = b[3];
-		}
+		const int hh = h < G ? h : 0; // unconditional loads (no branch around each)
+		const float *qp = q + (size_t)(g * G + hh) * D + piece * 8;
+		const float4_t a = *(const float4_t *)qp;
+		const float4_t b = *(const float4_t *)(qp + 4);
+		qr[h][0] = a[0], qr[h][1] = a[1], qr[h][2] = a[2], qr[h][3] = a[3];
+		qr[h][4] = b[0], qr[h][5] = b[1], qr[h][6] = b[2], qr[h][7] = b[3];
 	}
+	const int kv_len = step->kv_len;
+	if (t0 >= kv_len)
+		return; // whole workgroup exits before any barrier
+	const int nt = min(CHUNK, kv_len - t0);
+	const int ns = (kv_len + CHUNK - 1) / CHUNK;
 	const float sq = sqrtf((float)D);
 
-	// scores
+	// ---- scores: each lane's 8-element partial dots go to LDS; one thread per
+	// (head, key) then sums the D/8 partials in piece order (no shuffles)
 #pragma unroll
 	for (int i = 0; i < NK; ++i) {
 		const int tl = tl0 + i * RSTEP;
-		if (tl < nt) {
-			float kf[8];
-			WF16::unpack(kw[i], kf);
+		float kf[8];
+		WF16::unpack(kw[i], kf);
 #pragma unroll
-			for (int h = 0; h < GT; ++h) {
-				if (h < G) {
-					float d = 0.0f;
+		for (int h = 0; h < GT; ++h) {
+			float d = 0.0f;
 #pragma unroll
-					for (int e = 0; e < 8; ++e)
-						d = fmaf(qr[h][e], kf[e], d);
-					d = group_sum(d, LPK);
-					if (piece == 0)
-						sc[h][tl] = d / sq;
-				}
-			}
+			for (int e = 0; e < 8; ++e)
+				d = fmaf(qr[h][e], kf[e], d);
+			if (h < G && tl < CHUNK)
+				sp[(h * CHUNK + tl) * LPK + piece] = d;
 		}
 	}
 	__syncthreads();
+	for (int i = tid; i < G * CHUNK; i += ATTN_THREADS) {
+		const int h = i / CHUNK, t = i % CHUNK;
+		const float *pp = &sp[(h * CHUNK + t) * LPK];
+		float d = 0.0f;
+		if constexpr (LPK >= 4) {
+#pragma unroll
+			for (int j = 0; j < LPK; j += 4) {
+				const float4_t v = *(const float4_t *)(pp + j);
+				d += v[0] + v[1] + v[2] + v[3];
+			}
+		} else {
+#pragma unroll
+			for (int j = 0; j < LPK; ++j)
+				d += pp[j];
+		}
+		sc[h][t] = d / sq;
+	}
+	__syncthreads();
 
-	// chunk-local softmax statistics; wave w owns heads w, w+4, ...
+	// ---- chunk-local softmax statistics; wave w owns heads w, w+4, ... (DPP reductions)
 	for (int h = wave; h < G; h += ATTN_WAVES) {
 		float m = -FLT_MAX;
 		for (int t = lane; t < nt; t += 64)
@@ -111,7 +148,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_decode_kernel(
 		for (int t = lane; t < nt; t += 64) {
 			const float sv = sc[h][t];
 			if (att_dbg)
-				att_dbg[(size_t)(g * G + h) * max_seq_len + t0 + t] = sv;
+				st_sc1(att_dbg + (size_t)(g * G + h) * max_seq_len + t0 + t, sv);
 			const float p = expf(sv - m);
 			sc[h][t] = p;
 			l += p;
@@ -124,7 +161,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_decode_kernel(
 	}
 	__syncthreads();
 
-	// P.V from the prefetched V rows
+	// ---- P.V from the prefetched V rows; per-row-slot partials to LDS
 	float acc[GT][8];
 #pragma unroll
 	for (int h = 0; h < GT; ++h)
@@ -134,110 +171,95 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_decode_kernel(
 #pragma unroll
 	for (int i = 0; i < NK; ++i) {
 		const int tl = tl0 + i * RSTEP;
-		if (tl < nt) {
-			float vf[8];
-			WF16::unpack(vw[i], vf);
+		const float pv = tl < nt ? 1.0f : 0.0f;
+		float vf[8];
+		WF16::unpack(vw[i], vf);
 #pragma unroll
-			for (int h = 0; h < GT; ++h) {
-				if (h < G) {
-					const float p = sc[h][tl];
-#pragma unroll
-					for (int e = 0; e < 8; ++e)
-						acc[h][e] = fmaf(p, vf[e], acc[h][e]);
-				}
-			}
-		}
-	}
-#pragma unroll
-	for (int off = LPK; off < 64; off <<= 1)
-#pragma unroll
-		for (int h = 0; h < GT; ++h)
+		for (int h = 0; h < GT; ++h) {
+			const float p = tl < nt ? sc[h < G ? h : 0][tl < CHUNK ? tl : 0] : 0.0f;
 #pragma unroll
 			for (int e = 0; e < 8; ++e)
-				acc[h][e] += __shfl_xor(acc[h][e], off, 64);
-	if (sub == 0) {
+				acc[h][e] = fmaf(p, vf[e] * pv, acc[h][e]);
+		}
+	}
+	{
+		const int slot = wave * KPW + sub;
 #pragma unroll
-		for (int h = 0; h < GT; ++h)
-			if (h < G)
-#pragma unroll
-				for (int e = 0; e < 8; ++e)
-					red[wave][h][piece * 8 + e] = acc[h][e];
+		for (int h = 0; h < GT; ++h) {
+			if (h < G) {
+				float *rp = &red[slot][h][piece * 8];
+				*(float4_t *)rp = float4_t{acc[h][0], acc[h][1], acc[h][2], acc[h][3]};
+				*(float4_t *)(rp + 4) = float4_t{acc[h][4], acc[h][5], acc[h][6], acc[h][7]};
+			}
+		}
 	}
 	__syncthreads();
 
 	if (ns == 1) { // single chunk: normalise and write the head outputs directly
-		for (int i = threadIdx.x; i < G * D; i += ATTN_THREADS) {
+		for (int i = tid; i < G * D; i += ATTN_THREADS) {
 			const int h = i / D, d = i % D;
 			float o = 0.0f;
 #pragma unroll
-			for (int w = 0; w < ATTN_WAVES; ++w)
+			for (int w = 0; w < ATTN_WAVES * KPW; ++w)
 				o += red[w][h][d];
 			out[(size_t)(g * G + h) * D + d] = o / ml[h][1];
 		}
 		if (att_dbg) {
-			for (int i = threadIdx.x; i < G * nt; i += ATTN_THREADS) {
+			for (int i = tid; i < G * nt; i += ATTN_THREADS) {
 				const int h = i / nt, t = i % nt;
-				float *a = att_dbg + (size_t)(g * G + h) * max_seq_len + t;
-				*a = sc[h][t] / ml[h][1];
+				att_dbg[(size_t)(g * G + h) * max_seq_len + t] = sc[h][t] / ml[h][1];
 			}
 		}
 		return;
 	}
 
-	// publish this chunk's partial: o[D], m, l per head
-	for (int i = threadIdx.x; i < G * D; i += ATTN_THREADS) {
+	// ---- publish this chunk's partial (o[D], m, l per head) write-through
+	for (int i = tid; i < G * D; i += ATTN_THREADS) {
 		const int h = i / D, d = i % D;
 		float o = 0.0f;
 #pragma unroll
-		for (int w = 0; w < ATTN_WAVES; ++w)
+		for (int w = 0; w < ATTN_WAVES * KPW; ++w)
 			o += red[w][h][d];
-		part[((size_t)(g * G + h) * nsplit + s) * (D + 2) + d] = o;
+		st_sc1(part + ((size_t)(g * G + h) * nsplit + s) * (D + 2) + d, o);
 	}
-	if (threadIdx.x < G) {
-		float *pp = part + ((size_t)(g * G + threadIdx.x) * nsplit + s) * (D + 2);
-		pp[D] = ml[threadIdx.x][0];
-		pp[D + 1] = ml[threadIdx.x][1];
+	if (tid < G) {
+		float *pp = part + ((size_t)(g * G + tid) * nsplit + s) * (D + 2);
+		st_sc1(pp + D, ml[tid][0]);
+		st_sc1(pp + D + 1, ml[tid][1]);
 	}
-	// release: every storing wave drains, barrier, one agent-scope release, ticket
-	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // every storing wave drains
 	__syncthreads();
-	if (threadIdx.x == 0) {
-		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	if (tid == 0) {
 		const unsigned ticket = __hip_atomic_fetch_add(&counters[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 		const int last = ticket == (unsigned)(ns - 1);
-		if (last) {
-			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-			// reset for the next launch (kernel boundary orders it before reuse)
+		if (last) // reset for the next launch (the kernel boundary orders it)
 			__hip_atomic_store(&counters[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-		}
 		last_flag = last;
 	}
 	__syncthreads();
 	if (!last_flag)
 		return;
 
-	// last arriver: merge the ns chunk partials of heads g*G .. g*G+G-1 in chunk order
+	// ---- last arriver: merge the ns chunk partials of heads g*G .. in chunk order
 	for (int h = wave; h < G; h += ATTN_WAVES) {
 		const float *ph = part + (size_t)(g * G + h) * nsplit * (D + 2);
 		float M = -FLT_MAX;
-		for (int c = 0; c < ns; ++c)
-			M = fmaxf(M, ph[c * (D + 2) + D]);
+		for (int c = lane; c < ns; c += 64)
+			M = fmaxf(M, ld_sc1(ph + c * (D + 2) + D));
+		M = wave_max(M);
 		float L = 0.0f;
 		for (int c = 0; c < ns; ++c)
-			L += expf(ph[c * (D + 2) + D] - M) * ph[c * (D + 2) + D + 1];
+			L += expf(ld_sc1(ph + c * (D + 2) + D) - M) * ld_sc1(ph + c * (D + 2) + D + 1);
 		for (int d = lane; d < D; d += 64) {
 			float o = 0.0f;
 			for (int c = 0; c < ns; ++c)
-				o += expf(ph[c * (D + 2) + D] - M) * ph[c * (D + 2) + d];
+				o += expf(ld_sc1(ph + c * (D + 2) + D) - M) * ld_sc1(ph + c * (D + 2) + d);
 			out[(size_t)(g * G + h) * D + d] = o / L;
 		}
 		if (att_dbg) {
-			// raw scores were written by every chunk's workgroup before its release
 			for (int t = lane; t < kv_len; t += 64) {
 				float *a = att_dbg + (size_t)(g * G + h) * max_seq_len + t;
-				*a = expf(*a - M) / L;
+				*a = expf(ld_sc1(a) - M) / L;
 			}
 		}
 	}

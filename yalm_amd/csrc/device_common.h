@@ -26,17 +26,55 @@ struct StepState {
 	int pad[2];
 };
 
+// Cross-lane exchange without the LDS crossbar: __shfl_xor lowers to
+// ds_bpermute_b32 + an lgkmcnt(0) wait per step (~100+ cycles each, serialised),
+// which dominated the decode attention. DPP row permutations and gfx950's
+// v_permlane16/32_swap are plain VALU ops.
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+	return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+// partner values across rows: lane ^ 16 (permlane16_swap) and lane ^ 32 (permlane32_swap)
+__device__ __forceinline__ float xor16(float v) {
+	const unsigned u = __builtin_bit_cast(unsigned, v);
+	auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+	// r[0] holds the swapped odd rows of vdst, r[1] the swapped even rows of src:
+	// for every lane exactly one of them differs from u, and r[0]+r[1]-u is the partner.
+	return __builtin_bit_cast(float, (threadIdx.x & 16) ? r[0] : r[1]);
+}
+__device__ __forceinline__ float xor32(float v) {
+	const unsigned u = __builtin_bit_cast(unsigned, v);
+	auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+	return __builtin_bit_cast(float, (threadIdx.x & 32) ? r[0] : r[1]);
+}
+// Sum / max over each aligned row of 16 lanes (result in every lane of the row):
+// quad_perm [1,0,3,2] (xor 1), [2,3,0,1] (xor 2), row_half_mirror, row_mirror.
+__device__ __forceinline__ float row16_sum(float v) {
+	v += dpp<0xB1>(v);
+	v += dpp<0x4E>(v);
+	v += dpp<0x141>(v);
+	v += dpp<0x140>(v);
+	return v;
+}
+__device__ __forceinline__ float row16_max(float v) {
+	v = fmaxf(v, dpp<0xB1>(v));
+	v = fmaxf(v, dpp<0x4E>(v));
+	v = fmaxf(v, dpp<0x141>(v));
+	v = fmaxf(v, dpp<0x140>(v));
+	return v;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-	for (int off = 32; off > 0; off >>= 1)
-		v += __shfl_xor(v, off, 64);
+	v = row16_sum(v);
+	v += xor16(v);
+	v += xor32(v);
 	return v;
 }
 
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-	for (int off = 32; off > 0; off >>= 1)
-		v = fmaxf(v, __shfl_xor(v, off, 64));
+	v = row16_max(v);
+	v = fmaxf(v, xor16(v));
+	v = fmaxf(v, xor32(v));
 	return v;
 }
 

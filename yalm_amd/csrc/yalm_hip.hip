@@ -256,7 +256,7 @@ template <int D>
 static void launch_attn_D(int G, const float *q, const uint16_t *kc, const uint16_t *vc, const StepState *step,
                           int n_heads, int n_kv, int max_seq_len, int nsplit, float *part, unsigned *counters,
                           float *att, float *out, hipStream_t st) {
-	dim3 grid(n_kv, nsplit);
+	dim3 grid(n_kv, (max_seq_len + attn_chunk<D>() - 1) / attn_chunk<D>());
 #define YALM_ATTN(GT)                                                                                                  \
 	attn_decode_kernel<D, GT><<<grid, ATTN_THREADS, 0, st>>>(q, kc, vc, step, n_heads, n_kv, max_seq_len, nsplit,    \
 	                                                         part, counters, out, att)
@@ -271,8 +271,9 @@ static void launch_attn_D(int G, const float *q, const uint16_t *kc, const uint1
 #undef YALM_ATTN
 }
 
+// partial-buffer stride: chunks per kv head (the chunk is 64 keys for every head_dim)
 static int attn_nsplit(int max_seq_len) {
-	return (max_seq_len + ATTN_CHUNK - 1) / ATTN_CHUNK;
+	return (max_seq_len + attn_chunk<128>() - 1) / attn_chunk<128>();
 }
 
 // part: (n_heads, nsplit, head_dim + 2) floats; counters: n_kv zeroed words.
@@ -329,6 +330,7 @@ struct yalm_decoder_s {
 	GemvCfg gemv[GK_N];
 	bool eager = false;     // YALM_EAGER=1: launch kernels directly (profilers that mis-handle graph replay)
 	bool graph_sync = false; // YALM_GRAPH_SYNC=1: synchronise after every replay
+	int ablate = 0;          // YALM_ABLATE bitmask: skip qkv|attn|wo|glu|w2 (1|2|4|8|16), timing only
 	std::string kname;
 };
 
@@ -338,7 +340,8 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 	const yalm_block_weights &w = d->b[l];
 	hipStream_t st = d->stream;
 	const int q_dim = c.n_heads * c.head_dim, kv_dim = c.n_kv_heads * c.head_dim;
-	{
+	const int ab = d->ablate; // timing-only ablation mask (YALM_ABLATE): results are wrong when set
+	if (!(ab & 1)) {
 		PQKV<WT> p;
 		p.wq = (const char *)w.wq;
 		p.wk = (const char *)w.wk;
@@ -356,9 +359,10 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 		p.vcache = w.value_cache;
 		TRY((launch_gemv<WT, PQKV<WT>, true>(p, d->x, w.rms_att, c.norm_eps, GK_QKV, d->gemv[GK_QKV], st)));
 	}
-	TRY(launch_attn(c.head_dim, c.n_heads, c.n_kv_heads, d->q, w.key_cache, w.value_cache, d->step, c.max_seq_len,
-	                d->part, d->attn_counters, nullptr, d->xb2, st));
-	{
+	if (!(ab & 2))
+		TRY(launch_attn(c.head_dim, c.n_heads, c.n_kv_heads, d->q, w.key_cache, w.value_cache, d->step,
+		                c.max_seq_len, d->part, d->attn_counters, nullptr, d->xb2, st));
+	if (!(ab & 4)) {
 		PResidual<WT, 1> p;
 		p.W = (const char *)w.wo;
 		p.n = q_dim;
@@ -366,7 +370,8 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 		p.n_groups = c.dim;
 		TRY((launch_gemv<WT, PResidual<WT, 1>, false>(p, d->xb2, nullptr, 0.f, GK_WO, d->gemv[GK_WO], st)));
 	}
-	if (c.act == YALM_SILU) {
+	if (ab & 8) {
+	} else if (c.act == YALM_SILU) {
 		PGlu<WT, 1> p;
 		p.w1 = (const char *)w.w1;
 		p.w3 = (const char *)w.w3;
@@ -383,7 +388,7 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 		p.n_groups = c.hidden_dim;
 		TRY((launch_gemv<WT, PGlu<WT, 0>, true>(p, d->x, w.rms_ffn, c.norm_eps, GK_GLU, d->gemv[GK_GLU], st)));
 	}
-	{
+	if (!(ab & 16)) {
 		PResidual<WT, 1> p;
 		p.W = (const char *)w.w2;
 		p.n = c.hidden_dim;
@@ -538,6 +543,7 @@ extern "C" int yalm_decoder_create(const yalm_config *config, const yalm_model_w
 	d->tokens_cap = 1 << 16;
 	d->eager = getenv("YALM_EAGER") && atoi(getenv("YALM_EAGER")) != 0;
 	d->graph_sync = getenv("YALM_GRAPH_SYNC") && atoi(getenv("YALM_GRAPH_SYNC")) != 0;
+	d->ablate = getenv("YALM_ABLATE") ? atoi(getenv("YALM_ABLATE")) : 0;
 	if ((r = dalloc(d, (void **)&d->step, sizeof(StepState))) || (r = dalloc(d, (void **)&d->x, sizeof(float) * c.dim)) ||
 	    (r = dalloc(d, (void **)&d->q, sizeof(float) * q_dim)) ||
 	    (r = dalloc(d, (void **)&d->xb2, sizeof(float) * q_dim)) ||
