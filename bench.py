@@ -39,6 +39,27 @@ def parse():
     return ap.parse_args()
 
 
+def pmc_traffic(kernel_prefix, dtype):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3
+    --pmc FETCH_SIZE pass (profiles/*_pmc_fetch_size_glu.csv): median
+    FETCH_SIZE (KB) x 1024 x 2 — gfx950 counts half the bytes of 16 B/lane
+    streaming reads (MI355X_MICROARCH.md §HBM). None if no matching profile."""
+    import csv
+    import glob
+    import statistics
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_fetch_size_glu.csv")))
+    if not files or dtype != "fp16":
+        return None, None
+    rows = list(csv.DictReader(open(files[-1])))
+    vals = [float(r["Counter_Value"]) for r in rows
+            if r["Counter_Name"] == "FETCH_SIZE" and kernel_prefix.split("<")[0] in r["Kernel_Name"]
+            and "PGlu" in r["Kernel_Name"]]
+    if not vals:
+        return None, None
+    return int(statistics.median(vals) * 1024 * 2), os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(cfg, budget_s):
     """The CPU oracle (oracle/, restatement of the reference -d cpu path with
     its AVX2/F16C GEMV and OpenMP) on the same synthetic weights, timed on
@@ -144,6 +165,7 @@ def main():
     glu_bytes = 2 * cfg.hidden_dim * cfg.dim * wb + 2 * cfg.dim * 4 + cfg.hidden_dim * 4
     achieved = glu_bytes / (avg_ms * 1e-3) / 1e9
     kname = dec.kernel_name(KID)
+    traffic, traffic_src = pmc_traffic(kname, args.dtype)
 
     toks = args.steps * world
     value = toks / elapsed
@@ -190,7 +212,8 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
         },
         "cpu_baseline": None,
     }
