@@ -138,8 +138,10 @@ int yalm_get_logits(yalm_decoder d, float *host);
  * 5 = logits GEMV. Used by bench.py for the roofline of the dominant kernel. */
 int yalm_time_kernel(yalm_decoder d, int kernel_id, int iters, float *avg_ms);
 /* Override the GEMV launch geometry of one weight-streaming kernel kind
- * (0 = QKV, 1 = Wo, 2 = W1/W3, 3 = W2, 4 = logits): workgroup size 256|512,
- * unroll (chunks in flight per wave) 4|8, row groups per wave; 0 = automatic.
+ * (0 = QKV, 1 = Wo, 2 = W1/W3, 3 = W2, 4 = logits): workgroup size
+ * 256|512|1024, unroll (16-byte loads in flight per lane) 2|4|8, and `gpw` =
+ * workgroups per CU of the row-block kernel (row groups per wave of the legacy
+ * kernel under YALM_GEMV_LEGACY=1); 0 = automatic.
  * Drops captured graphs (re-captured on next use). Tuning/ablation hook. */
 int yalm_set_gemv_config(yalm_decoder d, int kind, int threads, int unroll, int gpw);
 /* Name of kernel_id's device function (to match rocprofv3 summaries). */

@@ -34,6 +34,11 @@ struct PStore {
 		if (lane < R)
 			out[g * R + lane] = acc[lane];
 	}
+	__device__ __forceinline__ void finish_all(int g, const float *acc) const {
+#pragma unroll
+		for (int r = 0; r < R; ++r)
+			out[g * R + r] = acc[r];
+	}
 };
 
 template <class WT, int R_>
@@ -50,6 +55,11 @@ struct PResidual {
 	__device__ __forceinline__ void finish(int g, const float *acc, int lane) const {
 		if (lane < R)
 			out[g * R + lane] += acc[lane];
+	}
+	__device__ __forceinline__ void finish_all(int g, const float *acc) const {
+#pragma unroll
+		for (int r = 0; r < R; ++r)
+			out[g * R + r] += acc[r];
 	}
 };
 
@@ -105,6 +115,7 @@ struct PQKV {
 			kcache[o + 1] = f2h(r1);
 		}
 	}
+	__device__ __forceinline__ void finish_all(int g, const float *acc) const { finish(g, acc, 0); }
 };
 
 template <class WT, int ACT>
@@ -122,6 +133,7 @@ struct PGlu {
 		if (lane == 0)
 			out[g] = act_fn<ACT>(acc[0]) * acc[1];
 	}
+	__device__ __forceinline__ void finish_all(int g, const float *acc) const { finish(g, acc, 0); }
 };
 
 // Rotate the attention-sink keys by one position (infer.cpp:303-317,
@@ -372,5 +384,110 @@ __global__ __launch_bounds__(THREADS) void gemv_stream_kernel(P p, const float *
 				}
 			}
 		}
+	}
+}
+
+// Row-block GEMV — the production path (n % (64 * EPL) == 0).
+//
+// One workgroup per CU (gridDim.x = NB ~ CU count): row group g belongs to
+// workgroup g % NB, so at every moment the chip streams ONE contiguous window
+// of rows (giving each CU a contiguous slice instead puts every CU on the same
+// HBM channels at once: tools/persist_bench.hip measured 3.2 vs 6.4 TB/s).
+// Inside the workgroup the (virtual row, 1-KB chunk) items of its groups are
+// dealt round-robin over the waves — balanced to one item whatever n is — and
+// each wave streams its items with U loads in flight. The refill of slot u is
+// issued unconditionally (past the end it re-reads a line of x, an L2 hit) so
+// hipcc's vmcnt bookkeeping stays static: with a conditional refill it emits
+// vmcnt(0) before every load and the pipeline collapses. x is staged (and
+// rmsnorm'ed) once per CU instead of once per small workgroup (1792 x 32 KB
+// of L2 reads for W1/W3 before). Row partials are wave-reduced (DPP), parked
+// in LDS per (row, wave) and summed in wave order by one thread per group,
+// which runs the policy epilogue (finish_all).
+template <class WT, class P, int U, bool NORM, int THREADS>
+__global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__restrict__ x,
+                                                          const float *__restrict__ normw, float eps) {
+	extern __shared__ __attribute__((aligned(16))) float xs[];
+	constexpr int R = P::R;
+	constexpr int EPL = WT::EPL;
+	constexpr int CH = YALM_WAVE * EPL;
+	constexpr size_t CHB = (size_t)CH * WT::BYTES;
+	constexpr int W = THREADS / YALM_WAVE;
+	const int n = p.n;
+	const int nch = n / CH;
+	const int NB = gridDim.x;
+	const int b = blockIdx.x;
+	const int lane = threadIdx.x & 63;
+	const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	const int ngl = b < p.n_groups ? (p.n_groups - 1 - b) / NB + 1 : 0; // groups of this workgroup
+	const int items = ngl * R * nch;
+	const int mine = items > wave ? (items - 1 - wave) / W + 1 : 0; // items wave, wave + W, ...
+	float *part = xs + ((n + 3) & ~3) + 64;                         // [ngl * R][W]
+	const size_t lane_off = (size_t)lane * EPL * WT::BYTES;
+	const char *dummy = (const char *)x + lane * 16;
+
+	auto advance = [&](int &vr, int &c) {
+		c += W;
+		while (c >= nch) {
+			c -= nch;
+			++vr;
+		}
+	};
+	auto iaddr = [&](int vr, int c) {
+		const int gl = vr / R, r = vr - gl * R;
+		return p.row(b + gl * NB, r) + (size_t)c * CHB + lane_off;
+	};
+
+	int ivr = wave / nch, ic = wave - (wave / nch) * nch; // issue cursor
+	const int vr0 = ivr, c0 = ic;
+	u32x4_t buf[U];
+#pragma unroll
+	for (int u = 0; u < U; ++u) {
+		buf[u] = load_nt16(u < mine ? iaddr(ivr, ic) : dummy);
+		advance(ivr, ic);
+	}
+	p.prologue();
+	for (int i = threadIdx.x; i < ngl * R * W; i += THREADS)
+		part[i] = 0.0f;
+	stage_x<NORM>(xs, x, normw, n, eps);
+
+	if (mine > 0) {
+		int cvr = vr0, cc = c0, cur = vr0; // consume cursor, row being accumulated
+		float acc[1] = {0.0f};
+		for (int k = 0; k < mine; k += U) {
+#pragma unroll
+			for (int u = 0; u < U; ++u) {
+				const int j = k + u;
+				if (j < mine) {
+					if (cvr != cur) {
+						const float s = wave_sum(acc[0]);
+						if (lane == 0)
+							part[cur * W + wave] = s;
+						acc[0] = 0.0f;
+						cur = cvr;
+					}
+					const u32x4_t wv[1] = {buf[u]};
+					fma_chunk<WT, 1>(acc, wv, xs + cc * CH + lane * EPL);
+					advance(cvr, cc);
+				}
+				buf[u] = load_nt16(j + U < mine ? iaddr(ivr, ic) : dummy);
+				advance(ivr, ic);
+			}
+		}
+		const float s = wave_sum(acc[0]);
+		if (lane == 0)
+			part[cur * W + wave] = s;
+	}
+	__syncthreads();
+	for (int gl = threadIdx.x; gl < ngl; gl += THREADS) {
+		float a[R];
+#pragma unroll
+		for (int r = 0; r < R; ++r) {
+			float t = 0.0f;
+#pragma unroll
+			for (int w = 0; w < W; ++w)
+				t += part[(gl * R + r) * W + w];
+			a[r] = t;
+		}
+		p.finish_all(b + gl * NB, a);
 	}
 }

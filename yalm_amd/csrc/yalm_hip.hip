@@ -220,6 +220,57 @@ static int launch_stream(const P &p, const float *x, const float *normw, float e
 	return YALM_OK;
 }
 
+// Row-block geometry (gemv_rb_kernel): `gpw` = workgroups per CU (default 1),
+// threads 512 (8 waves), U = 8 loads in flight per wave.
+template <class WT, class P, bool NORM, int THREADS, int U>
+static int launch_rb_t(const P &p, const float *x, const float *normw, float eps, int wpc, hipStream_t st) {
+	auto kern = gemv_rb_kernel<WT, P, U, NORM, THREADS>;
+	const int nb = std::max(1, std::min(p.n_groups, device_cu_count() * std::max(1, wpc)));
+	const int ngl = (p.n_groups + nb - 1) / nb;
+	const size_t lds = ((size_t)((p.n + 3) & ~3) + 64 + (size_t)ngl * P::R * (THREADS / YALM_WAVE)) * sizeof(float);
+	if (lds > 65536)
+		HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+	hipLaunchKernelGGL(kern, dim3(nb), dim3(THREADS), lds, st, p, x, normw, eps);
+	HIPCHK(hipGetLastError());
+	return YALM_OK;
+}
+
+// Per-kind defaults from tools/sweep_gemv.py on MI355X (profiles/r1_sweep_rb.txt):
+// 512 threads and U = 4 everywhere; QKV 2 and logits 4 workgroups per CU.
+static GemvCfg default_rb_cfg(int kind) {
+	if (kind == GK_QKV)
+		return GemvCfg{512, 4, 2};
+	if (kind == GK_CLS)
+		return GemvCfg{512, 4, 4};
+	return GemvCfg{512, 4, 1};
+}
+
+template <class WT, class P, bool NORM, int THREADS>
+static int launch_rb_u(const P &p, const float *x, const float *normw, float eps, int U, int wpc, hipStream_t st) {
+	switch (U) {
+	case 2:
+		return launch_rb_t<WT, P, NORM, THREADS, 2>(p, x, normw, eps, wpc, st);
+	case 8:
+		return launch_rb_t<WT, P, NORM, THREADS, 8>(p, x, normw, eps, wpc, st);
+	default:
+		return launch_rb_t<WT, P, NORM, THREADS, 4>(p, x, normw, eps, wpc, st);
+	}
+}
+
+template <class WT, class P, bool NORM>
+static int launch_rb(const P &p, const float *x, const float *normw, float eps, int kind, GemvCfg want,
+                     hipStream_t st) {
+	const GemvCfg def = default_rb_cfg(kind);
+	const int threads = want.threads ? want.threads : def.threads;
+	const int U = want.U ? want.U : def.U;
+	const int wpc = want.gpw ? want.gpw : def.gpw;
+	if (threads == 256)
+		return launch_rb_u<WT, P, NORM, 256>(p, x, normw, eps, U, wpc, st);
+	if (threads == 1024)
+		return launch_rb_u<WT, P, NORM, 1024>(p, x, normw, eps, U, wpc, st);
+	return launch_rb_u<WT, P, NORM, 512>(p, x, normw, eps, U, wpc, st);
+}
+
 template <class WT, class P, bool NORM>
 static int launch_gemv(const P &p, const float *x, const float *normw, float eps, int kind, GemvCfg want,
                        hipStream_t st) {
@@ -234,6 +285,9 @@ static int launch_gemv(const P &p, const float *x, const float *normw, float eps
 		HIPCHK(hipGetLastError());
 		return YALM_OK;
 	}
+	static const bool legacy = getenv("YALM_GEMV_LEGACY") && atoi(getenv("YALM_GEMV_LEGACY")) != 0;
+	if (!legacy)
+		return launch_rb<WT, P, NORM>(p, x, normw, eps, kind, want, st);
 	static const bool balanced = getenv("YALM_GEMV_BALANCED") && atoi(getenv("YALM_GEMV_BALANCED")) != 0;
 	const GemvCfg def = balanced ? balanced_gemv_cfg(p.n_groups, lds, want) : default_gemv_cfg(kind);
 	GemvCfg c;
@@ -761,8 +815,8 @@ extern "C" int yalm_time_kernel(yalm_decoder d, int kernel_id, int iters, float 
 
 extern "C" int yalm_set_gemv_config(yalm_decoder d, int kind, int threads, int unroll, int gpw) {
 	ARGCHK(d && kind >= 0 && kind < GK_N, "bad decoder/kind");
-	ARGCHK(threads == 0 || threads == 256 || threads == 512, "threads must be 0, 256 or 512");
-	ARGCHK(unroll == 0 || unroll == 4 || unroll == 8, "unroll must be 0, 4 or 8");
+	ARGCHK(threads == 0 || threads == 256 || threads == 512 || threads == 1024, "threads must be 0, 256, 512 or 1024");
+	ARGCHK(unroll == 0 || unroll == 2 || unroll == 4 || unroll == 8, "unroll must be 0, 2, 4 or 8");
 	ARGCHK(gpw >= 0, "gpw must be >= 0");
 	d->gemv[kind] = GemvCfg{threads, unroll, gpw};
 	// captured graphs bake the old geometry: drop them
@@ -783,22 +837,24 @@ extern "C" const char *yalm_kernel_name(yalm_decoder d, int kernel_id) {
 		return "";
 	const char *wt = d->c.weight_dtype == YALM_F32 ? "WF32" : d->c.weight_dtype == YALM_F16 ? "WF16" : "WF8";
 	std::string s;
+	static const bool legacy = getenv("YALM_GEMV_LEGACY") && atoi(getenv("YALM_GEMV_LEGACY")) != 0;
+	const std::string gk = legacy ? "gemv_stream_kernel<" : "gemv_rb_kernel<";
 	switch (kernel_id) {
 	case 0:
-		s = std::string("gemv_stream_kernel<") + wt + ", PQKV<";
+		s = gk + wt + ", PQKV<";
 		break;
 	case 1:
 		s = "attn_decode_kernel<";
 		break;
 	case 2:
 	case 4:
-		s = std::string("gemv_stream_kernel<") + wt + ", PResidual<";
+		s = gk + wt + ", PResidual<";
 		break;
 	case 3:
-		s = std::string("gemv_stream_kernel<") + wt + ", PGlu<";
+		s = gk + wt + ", PGlu<";
 		break;
 	case 5:
-		s = std::string("gemv_stream_kernel<") + wt + ", PStore<";
+		s = gk + wt + ", PStore<";
 		break;
 	default:
 		s = "";
