@@ -196,6 +196,123 @@ __global__ __launch_bounds__(THR, 1) void persist_kernel(Args a) {
 		a.out[0] = acc;
 }
 
+// Coordinator variant: wave 0 streams nothing — it publishes, arrives and
+// polls with no weight loads queued ahead of its poll (in-order vmcnt: a poll
+// behind U prefetch loads returns only after them). Waves 1..7 stream and keep
+// their refills running across every seam (the prefetch).
+template <int U>
+__global__ __launch_bounds__(THR, 1) void persist_coord_kernel(Args a) {
+	__shared__ __attribute__((aligned(16))) float vec[14336];
+	__shared__ unsigned sh_epoch;
+	constexpr int NS = NWAVE - 1;
+	const int w = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+	const int v = __builtin_amdgcn_readfirstlane(tid >> 6);
+	if (tid == 0)
+		sh_epoch = ld_sc1u(a.epoch);
+	__syncthreads();
+	const unsigned E = sh_epoch;
+	const unsigned seams_per_launch = 5 * a.nl - 1;
+	unsigned seam = 0;
+	unsigned acc = 0;
+	auto next_target = [&]() { return 256u * (E * seams_per_launch + (++seam)); };
+	auto gather = [&](int n) {
+		for (int i = tid * 4; i < n; i += THR * 4)
+			*(f32x4 *)&vec[i] = ld_sc1x4(a.vec, i * 4);
+		__syncthreads();
+	};
+	// per-phase item counts of this wave (items s, s+NS, ... of the WG's phase slice)
+	int NP[NPH], cum[NPH + 1];
+	cum[0] = 0;
+	for (int p = 0; p < NPH; ++p) {
+		const int tot = (int)(a.per_wg[p] / ITEM);
+		NP[p] = v == 0 ? 0 : (tot > v - 1 ? (tot - 1 - (v - 1)) / NS + 1 : 0);
+		cum[p + 1] = cum[p] + NP[p];
+	}
+	const int per_layer = cum[NPH];
+	const int T = per_layer * a.nl;
+	auto addr = [&](int t) {
+		const int li = t / per_layer, r = t - li * per_layer;
+		const int p = r < cum[1] ? 0 : r < cum[2] ? 1 : r < cum[3] ? 2 : 3;
+		const int it = (v - 1) + NS * (r - cum[p]); // item within the WG slice
+		const int blk = it / NWAVE, sub = it - blk * NWAVE;
+		return a.base + (size_t)(a.l0 + li) * a.layer_bytes + a.off[p] + ((size_t)(blk * NWG + w) * NWAVE + sub) * ITEM +
+		       lane * 16;
+	};
+	const char *dummy = (const char *)a.vec + lane * 16;
+	// seam sequence identical for all waves: after each phase except the last of the launch
+	auto do_seam = [&](int p_done, int np) {
+		// streamers: partials would go to LDS here
+		__syncthreads();
+		if (v == 0) {
+			const int outs = (p_done == 2 ? 14336 : 4096) / NWG;
+			if (lane < outs)
+				st_sc1f(a.vec + w * outs + lane, (float)(acc & 0xff));
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			if (lane == 0)
+				__hip_atomic_fetch_add(a.counters + (w & 7) * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		}
+		seam_wait(a, next_target(), tid);
+		if (np == 1) {
+			if (w < ATT_WGS) {
+				float s = 0.f;
+				const float *kb = (const float *)(a.kv + (size_t)w * ATT_BYTES);
+				for (int i = tid * 4; i < ATT_BYTES / 4; i += THR * 4) {
+					f32x4 tt = ld_sc1x4(kb, i * 4);
+					s += tt[0] + tt[1] + tt[2] + tt[3];
+				}
+				if (tid == 0)
+					st_sc1f(a.vec + w, s);
+				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			}
+			__syncthreads();
+			if (tid == 0)
+				__hip_atomic_fetch_add(a.counters + (w & 7) * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			seam_wait(a, next_target(), tid);
+		}
+		gather(a.gather[np]);
+	};
+
+	gather(a.gather[0]);
+	if (v == 0) {
+		// coordinator: walk the same seam sequence
+		for (int li = 0; li < a.nl; ++li)
+			for (int p = 0; p < NPH; ++p)
+				if (!(li == a.nl - 1 && p == NPH - 1))
+					do_seam(p, (p + 1) % NPH);
+	} else {
+		u32x4 buf[U];
+#pragma unroll
+		for (int u = 0; u < U; ++u)
+			buf[u] = ldnt(u < T ? addr(u) : dummy);
+		int r = 0;
+		for (int k = 0; k < T; k += U) {
+#pragma unroll
+			for (int u = 0; u < U; ++u) {
+				const int t = k + u;
+				if (t < T) {
+					if (r == per_layer)
+						r = 0;
+					const int p = r < cum[1] ? 0 : r < cum[2] ? 1 : r < cum[3] ? 2 : 3; // (every phase non-empty here)
+					acc ^= buf[u][0] ^ buf[u][1] ^ buf[u][2] ^ buf[u][3];
+					++r;
+					if (r == cum[p + 1] && t + 1 < T) // last item of this phase: seam after it
+						do_seam(p, (p + 1) % NPH);
+				}
+				buf[u] = ldnt(t + U < T ? addr(t + U) : dummy);
+			}
+		}
+	}
+	acc += __float_as_uint(vec[(tid * 7) % 4096]);
+	__syncthreads();
+	if (tid == 0) {
+		const unsigned t = __hip_atomic_fetch_add(a.endc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		if (t == 256u * (E + 1) - 1)
+			__hip_atomic_fetch_add(a.epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	}
+	if (acc == 0x12345678u)
+		a.out[0] = acc;
+}
+
 // pure streaming in the persistent geometry: the same item stream, no seams
 template <int U>
 __global__ __launch_bounds__(THR, 1) void persist_noseam_kernel(Args a) {
@@ -392,6 +509,36 @@ int main(int argc, char **argv) {
 		noseam(persist_noseam_kernel<8>, 8);
 		noseam(persist_noseam_kernel<16>, 16);
 	}
+	auto runc = [&](auto kern, int U, bool ALL) {
+		CHK(hipMemset(ctr, 0, 4096));
+		float ms = timeit([&] {
+			if (ALL) {
+				a.l0 = 0, a.nl = L;
+				kern<<<NWG, THR>>>(a);
+			} else {
+				for (int l = 0; l < L; ++l) {
+					a.l0 = l, a.nl = 1;
+					kern<<<NWG, THR>>>(a);
+				}
+			}
+		});
+		unsigned err;
+		CHK(hipMemcpy(&err, a.err, 4, hipMemcpyDeviceToHost));
+		char nm[96];
+		snprintf(nm, sizeof nm, "coord%s U=%d", ALL ? "-all" : "", U);
+		report(nm, ms);
+		if (err) {
+			printf("  SEAM TIMEOUT err=%x\n", err);
+			exit(1);
+		}
+	};
+	runc(persist_coord_kernel<4>, 4, false);
+	runc(persist_coord_kernel<8>, 8, false);
+	runc(persist_coord_kernel<16>, 16, false);
+	runc(persist_coord_kernel<4>, 4, true);
+	runc(persist_coord_kernel<8>, 8, true);
+	runc(persist_coord_kernel<16>, 16, true);
+	runc(persist_coord_kernel<24>, 24, true);
 	RUNP(8, false, true, false);
 	RUNP(8, true, true, false);
 	RUNP(16, true, true, false);

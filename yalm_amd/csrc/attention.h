@@ -64,8 +64,8 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_decode_kernel(
 	__shared__ int last_flag;
 
 	const int g = blockIdx.x;
-	const int s = blockIdx.y;
-	const int t0 = s * CHUNK;
+	const int s0 = blockIdx.y;
+	const int S = gridDim.y;
 	const int G = n_heads / n_kv_heads;
 	const int kv_dim = n_kv_heads * D;
 	const int lane = threadIdx.x & 63;
@@ -75,15 +75,18 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_decode_kernel(
 	const int piece = lane % LPK;
 	const int tl0 = wave * KPW + sub;
 
-	// ---- speculative loads (chunk rows clamped to the cache, q, step) in flight together
-	u32x4_t kw[NK], vw[NK];
+	auto load_kv = [&](int t0, u32x4_t (&kw)[NK], u32x4_t (&vw)[NK]) {
 #pragma unroll
-	for (int i = 0; i < NK; ++i) {
-		const int t = min(t0 + tl0 + i * RSTEP, max_seq_len - 1);
-		const size_t off = (size_t)t * kv_dim + g * D + piece * 8;
-		kw[i] = load16(kc + off);
-		vw[i] = load16(vc + off);
-	}
+		for (int i = 0; i < NK; ++i) {
+			const int t = min(t0 + tl0 + i * RSTEP, max_seq_len - 1);
+			const size_t off = (size_t)t * kv_dim + g * D + piece * 8;
+			kw[i] = load16(kc + off);
+			vw[i] = load16(vc + off);
+		}
+	};
+	// ---- speculative loads of the first chunk (rows clamped to the cache), q and step in flight together
+	u32x4_t kw[NK], vw[NK];
+	load_kv(s0 * CHUNK, kw, vw);
 	float qr[GT][8];
 #pragma unroll
 	for (int h = 0; h < GT; ++h) {
@@ -95,143 +98,152 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_decode_kernel(
 		qr[h][4] = b[0], qr[h][5] = b[1], qr[h][6] = b[2], qr[h][7] = b[3];
 	}
 	const int kv_len = step->kv_len;
-	if (t0 >= kv_len)
+	if (s0 * CHUNK >= kv_len)
 		return; // whole workgroup exits before any barrier
-	const int nt = min(CHUNK, kv_len - t0);
 	const int ns = (kv_len + CHUNK - 1) / CHUNK;
 	const float sq = sqrtf((float)D);
 
-	// ---- scores: each lane's 8-element partial dots go to LDS; one thread per
-	// (head, key) then sums the D/8 partials in piece order (no shuffles)
+	// chunks s0, s0 + S, ... (S = gridDim.y splits; one pass for kv_len <= S * CHUNK)
+	for (int cidx = s0; cidx < ns; cidx += S) {
+		const int t0 = cidx * CHUNK;
+		if (cidx != s0)
+			load_kv(t0, kw, vw);
+		const int nt = min(CHUNK, kv_len - t0);
+
+		// ---- scores: each lane's 8-element partial dots go to LDS; one thread per
+		// (head, key) then sums the D/8 partials in piece order (no shuffles)
 #pragma unroll
-	for (int i = 0; i < NK; ++i) {
-		const int tl = tl0 + i * RSTEP;
-		float kf[8];
-		WF16::unpack(kw[i], kf);
+		for (int i = 0; i < NK; ++i) {
+			const int tl = tl0 + i * RSTEP;
+			float kf[8];
+			WF16::unpack(kw[i], kf);
 #pragma unroll
-		for (int h = 0; h < GT; ++h) {
+			for (int h = 0; h < GT; ++h) {
+				float d = 0.0f;
+#pragma unroll
+				for (int e = 0; e < 8; ++e)
+					d = fmaf(qr[h][e], kf[e], d);
+				if (h < G && tl < CHUNK)
+					sp[(h * CHUNK + tl) * LPK + piece] = d;
+			}
+		}
+		__syncthreads();
+		for (int i = tid; i < G * CHUNK; i += ATTN_THREADS) {
+			const int h = i / CHUNK, t = i % CHUNK;
+			const float *pp = &sp[(h * CHUNK + t) * LPK];
 			float d = 0.0f;
+			if constexpr (LPK >= 4) {
 #pragma unroll
-			for (int e = 0; e < 8; ++e)
-				d = fmaf(qr[h][e], kf[e], d);
-			if (h < G && tl < CHUNK)
-				sp[(h * CHUNK + tl) * LPK + piece] = d;
-		}
-	}
-	__syncthreads();
-	for (int i = tid; i < G * CHUNK; i += ATTN_THREADS) {
-		const int h = i / CHUNK, t = i % CHUNK;
-		const float *pp = &sp[(h * CHUNK + t) * LPK];
-		float d = 0.0f;
-		if constexpr (LPK >= 4) {
+				for (int j = 0; j < LPK; j += 4) {
+					const float4_t v = *(const float4_t *)(pp + j);
+					d += v[0] + v[1] + v[2] + v[3];
+				}
+			} else {
 #pragma unroll
-			for (int j = 0; j < LPK; j += 4) {
-				const float4_t v = *(const float4_t *)(pp + j);
-				d += v[0] + v[1] + v[2] + v[3];
+				for (int j = 0; j < LPK; ++j)
+					d += pp[j];
 			}
-		} else {
-#pragma unroll
-			for (int j = 0; j < LPK; ++j)
-				d += pp[j];
+			sc[h][t] = d / sq;
 		}
-		sc[h][t] = d / sq;
-	}
-	__syncthreads();
+		__syncthreads();
 
-	// ---- chunk-local softmax statistics; wave w owns heads w, w+4, ... (DPP reductions)
-	for (int h = wave; h < G; h += ATTN_WAVES) {
-		float m = -FLT_MAX;
-		for (int t = lane; t < nt; t += 64)
-			m = fmaxf(m, sc[h][t]);
-		m = wave_max(m);
-		float l = 0.0f;
-		for (int t = lane; t < nt; t += 64) {
-			const float sv = sc[h][t];
-			if (att_dbg)
-				st_sc1(att_dbg + (size_t)(g * G + h) * max_seq_len + t0 + t, sv);
-			const float p = expf(sv - m);
-			sc[h][t] = p;
-			l += p;
-		}
-		l = wave_sum(l);
-		if (lane == 0) {
-			ml[h][0] = m;
-			ml[h][1] = l;
-		}
-	}
-	__syncthreads();
-
-	// ---- P.V from the prefetched V rows; per-row-slot partials to LDS
-	float acc[GT][8];
-#pragma unroll
-	for (int h = 0; h < GT; ++h)
-#pragma unroll
-		for (int e = 0; e < 8; ++e)
-			acc[h][e] = 0.0f;
-#pragma unroll
-	for (int i = 0; i < NK; ++i) {
-		const int tl = tl0 + i * RSTEP;
-		const float pv = tl < nt ? 1.0f : 0.0f;
-		float vf[8];
-		WF16::unpack(vw[i], vf);
-#pragma unroll
-		for (int h = 0; h < GT; ++h) {
-			const float p = tl < nt ? sc[h < G ? h : 0][tl < CHUNK ? tl : 0] : 0.0f;
-#pragma unroll
-			for (int e = 0; e < 8; ++e)
-				acc[h][e] = fmaf(p, vf[e] * pv, acc[h][e]);
-		}
-	}
-	{
-		const int slot = wave * KPW + sub;
-#pragma unroll
-		for (int h = 0; h < GT; ++h) {
-			if (h < G) {
-				float *rp = &red[slot][h][piece * 8];
-				*(float4_t *)rp = float4_t{acc[h][0], acc[h][1], acc[h][2], acc[h][3]};
-				*(float4_t *)(rp + 4) = float4_t{acc[h][4], acc[h][5], acc[h][6], acc[h][7]};
+		// ---- chunk-local softmax statistics; wave w owns heads w, w+4, ... (DPP reductions)
+		for (int h = wave; h < G; h += ATTN_WAVES) {
+			float m = -FLT_MAX;
+			for (int t = lane; t < nt; t += 64)
+				m = fmaxf(m, sc[h][t]);
+			m = wave_max(m);
+			float l = 0.0f;
+			for (int t = lane; t < nt; t += 64) {
+				const float sv = sc[h][t];
+				if (att_dbg)
+					st_sc1(att_dbg + (size_t)(g * G + h) * max_seq_len + t0 + t, sv);
+				const float p = expf(sv - m);
+				sc[h][t] = p;
+				l += p;
+			}
+			l = wave_sum(l);
+			if (lane == 0) {
+				ml[h][0] = m;
+				ml[h][1] = l;
 			}
 		}
-	}
-	__syncthreads();
+		__syncthreads();
 
-	if (ns == 1) { // single chunk: normalise and write the head outputs directly
+		// ---- P.V from the loaded V rows; per-row-slot partials to LDS
+		float acc[GT][8];
+#pragma unroll
+		for (int h = 0; h < GT; ++h)
+#pragma unroll
+			for (int e = 0; e < 8; ++e)
+				acc[h][e] = 0.0f;
+#pragma unroll
+		for (int i = 0; i < NK; ++i) {
+			const int tl = tl0 + i * RSTEP;
+			const float pv = tl < nt ? 1.0f : 0.0f;
+			float vf[8];
+			WF16::unpack(vw[i], vf);
+#pragma unroll
+			for (int h = 0; h < GT; ++h) {
+				const float p = tl < nt ? sc[h < G ? h : 0][tl < CHUNK ? tl : 0] : 0.0f;
+#pragma unroll
+				for (int e = 0; e < 8; ++e)
+					acc[h][e] = fmaf(p, vf[e] * pv, acc[h][e]);
+			}
+		}
+		{
+			const int slot = wave * KPW + sub;
+#pragma unroll
+			for (int h = 0; h < GT; ++h) {
+				if (h < G) {
+					float *rp = &red[slot][h][piece * 8];
+					*(float4_t *)rp = float4_t{acc[h][0], acc[h][1], acc[h][2], acc[h][3]};
+					*(float4_t *)(rp + 4) = float4_t{acc[h][4], acc[h][5], acc[h][6], acc[h][7]};
+				}
+			}
+		}
+		__syncthreads();
+
+		if (ns == 1) { // single chunk: normalise and write the head outputs directly
+			for (int i = tid; i < G * D; i += ATTN_THREADS) {
+				const int h = i / D, d = i % D;
+				float o = 0.0f;
+#pragma unroll
+				for (int w = 0; w < ATTN_WAVES * KPW; ++w)
+					o += red[w][h][d];
+				out[(size_t)(g * G + h) * D + d] = o / ml[h][1];
+			}
+			if (att_dbg) {
+				for (int i = tid; i < G * nt; i += ATTN_THREADS) {
+					const int h = i / nt, t = i % nt;
+					att_dbg[(size_t)(g * G + h) * max_seq_len + t] = sc[h][t] / ml[h][1];
+				}
+			}
+			return;
+		}
+
+		// ---- publish this chunk's partial (o[D], m, l per head) write-through
 		for (int i = tid; i < G * D; i += ATTN_THREADS) {
 			const int h = i / D, d = i % D;
 			float o = 0.0f;
 #pragma unroll
 			for (int w = 0; w < ATTN_WAVES * KPW; ++w)
 				o += red[w][h][d];
-			out[(size_t)(g * G + h) * D + d] = o / ml[h][1];
+			st_sc1(part + ((size_t)(g * G + h) * nsplit + cidx) * (D + 2) + d, o);
 		}
-		if (att_dbg) {
-			for (int i = tid; i < G * nt; i += ATTN_THREADS) {
-				const int h = i / nt, t = i % nt;
-				att_dbg[(size_t)(g * G + h) * max_seq_len + t] = sc[h][t] / ml[h][1];
-			}
+		if (tid < G) {
+			float *pp = part + ((size_t)(g * G + tid) * nsplit + cidx) * (D + 2);
+			st_sc1(pp + D, ml[tid][0]);
+			st_sc1(pp + D + 1, ml[tid][1]);
 		}
-		return;
-	}
-
-	// ---- publish this chunk's partial (o[D], m, l per head) write-through
-	for (int i = tid; i < G * D; i += ATTN_THREADS) {
-		const int h = i / D, d = i % D;
-		float o = 0.0f;
-#pragma unroll
-		for (int w = 0; w < ATTN_WAVES * KPW; ++w)
-			o += red[w][h][d];
-		st_sc1(part + ((size_t)(g * G + h) * nsplit + s) * (D + 2) + d, o);
-	}
-	if (tid < G) {
-		float *pp = part + ((size_t)(g * G + tid) * nsplit + s) * (D + 2);
-		st_sc1(pp + D, ml[tid][0]);
-		st_sc1(pp + D + 1, ml[tid][1]);
+		__syncthreads(); // LDS (sp, sc, ml, red) reused by the next chunk
 	}
 	asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // every storing wave drains
 	__syncthreads();
 	if (tid == 0) {
+		const int arrivals = min(ns, S); // workgroups with at least one chunk
 		const unsigned ticket = __hip_atomic_fetch_add(&counters[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-		const int last = ticket == (unsigned)(ns - 1);
+		const int last = ticket == (unsigned)(arrivals - 1);
 		if (last) // reset for the next launch (the kernel boundary orders it)
 			__hip_atomic_store(&counters[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 		last_flag = last;
@@ -240,21 +252,57 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_decode_kernel(
 	if (!last_flag)
 		return;
 
-	// ---- last arriver: merge the ns chunk partials of heads g*G .. in chunk order
+	// ---- last arriver: merge the ns chunk partials of heads g*G .. in chunk order.
+	// Batches of MB chunks: every (m, l, o[d]) load of a batch is issued before any
+	// is used (one L2 round trip per batch instead of one per chunk), merged with
+	// the online rescaling of flash-decoding; one batch covers kv_len <= 1024.
+	constexpr int MB = 16;
+	constexpr int DPL = D >= 64 ? D / 64 : 1; // dims per lane
 	for (int h = wave; h < G; h += ATTN_WAVES) {
 		const float *ph = part + (size_t)(g * G + h) * nsplit * (D + 2);
-		float M = -FLT_MAX;
-		for (int c = lane; c < ns; c += 64)
-			M = fmaxf(M, ld_sc1(ph + c * (D + 2) + D));
-		M = wave_max(M);
-		float L = 0.0f;
-		for (int c = 0; c < ns; ++c)
-			L += expf(ld_sc1(ph + c * (D + 2) + D) - M) * ld_sc1(ph + c * (D + 2) + D + 1);
-		for (int d = lane; d < D; d += 64) {
-			float o = 0.0f;
-			for (int c = 0; c < ns; ++c)
-				o += expf(ld_sc1(ph + c * (D + 2) + D) - M) * ld_sc1(ph + c * (D + 2) + d);
-			out[(size_t)(g * G + h) * D + d] = o / L;
+		float M = -FLT_MAX, L = 0.0f, o[DPL];
+#pragma unroll
+		for (int k = 0; k < DPL; ++k)
+			o[k] = 0.0f;
+		const bool dl = lane < D; // lanes past D (D < 64) only follow along
+		for (int c0 = 0; c0 < ns; c0 += MB) {
+			float mb[MB], lb[MB], ob[MB][DPL];
+#pragma unroll
+			for (int j = 0; j < MB; ++j) {
+				const int c = min(c0 + j, ns - 1);
+				const float *pc = ph + c * (D + 2);
+				mb[j] = ld_sc1(pc + D);
+				lb[j] = ld_sc1(pc + D + 1);
+#pragma unroll
+				for (int k = 0; k < DPL; ++k)
+					ob[j][k] = dl ? ld_sc1(pc + lane + 64 * k) : 0.0f;
+			}
+			float Mn = M;
+#pragma unroll
+			for (int j = 0; j < MB; ++j)
+				if (c0 + j < ns)
+					Mn = fmaxf(Mn, mb[j]);
+			const float r = expf(M - Mn); // 0 on the first batch (M = -FLT_MAX)
+			L *= r;
+#pragma unroll
+			for (int k = 0; k < DPL; ++k)
+				o[k] *= r;
+#pragma unroll
+			for (int j = 0; j < MB; ++j) {
+				if (c0 + j < ns) {
+					const float w = expf(mb[j] - Mn);
+					L += w * lb[j];
+#pragma unroll
+					for (int k = 0; k < DPL; ++k)
+						o[k] += w * ob[j][k];
+				}
+			}
+			M = Mn;
+		}
+		if (dl) {
+#pragma unroll
+			for (int k = 0; k < DPL; ++k)
+				out[(size_t)(g * G + h) * D + lane + 64 * k] = o[k] / L;
 		}
 		if (att_dbg) {
 			for (int t = lane; t < kv_len; t += 64) {

@@ -310,7 +310,12 @@ template <int D>
 static void launch_attn_D(int G, const float *q, const uint16_t *kc, const uint16_t *vc, const StepState *step,
                           int n_heads, int n_kv, int max_seq_len, int nsplit, float *part, unsigned *counters,
                           float *att, float *out, hipStream_t st) {
-	dim3 grid(n_kv, (max_seq_len + attn_chunk<D>() - 1) / attn_chunk<D>());
+	// S key-chunk splits per kv head, each workgroup looping over chunks s, s + S, ...: a grid
+	// sized for max_seq_len would issue the speculative first-chunk loads of every idle
+	// workgroup (15.6 MB of dead KV reads per layer at max_seq_len 4096, kv_len ~150).
+	static const int splits = getenv("YALM_ATTN_SPLITS") ? std::max(1, atoi(getenv("YALM_ATTN_SPLITS"))) : 32;
+	const int nchunks = (max_seq_len + attn_chunk<D>() - 1) / attn_chunk<D>();
+	dim3 grid(n_kv, std::min(nchunks, splits));
 #define YALM_ATTN(GT)                                                                                                  \
 	attn_decode_kernel<D, GT><<<grid, ATTN_THREADS, 0, st>>>(q, kc, vc, step, n_heads, n_kv, max_seq_len, nsplit,    \
 	                                                         part, counters, out, att)
