@@ -382,6 +382,99 @@ __global__ __launch_bounds__(256) void att_kernel(const char *kv, float *vec) {
 		vec[blockIdx.x] = s;
 }
 
+// ---- overlapped launches: kernel k runs on stream k % 2, so it is dispatched
+// while kernel k-1 still runs; it issues its first U weight loads, then waits
+// for k-1's arrival counter (sc1 poll by one lane), gathers the hand-off
+// vector with sc1 loads and streams the rest. Completion: sc1 stores,
+// vmcnt(0), one agent-scope add per workgroup.
+template <int U, int SLEEP>
+__global__ __launch_bounds__(512) void chain_kernel(const char *p, size_t bytes, int k, unsigned *counters, int nb_prev,
+                                                    float *vec, int gather, unsigned *err, unsigned *out) {
+	__shared__ __attribute__((aligned(16))) float xs[14336];
+	const int w = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+	const int v = __builtin_amdgcn_readfirstlane(tid >> 6);
+	const int nb = gridDim.x;
+	// items: 1 KB, block j*nb + w (8 KB) split over the 8 waves
+	const int nblk = (int)(bytes / 8192);
+	const int mine = (nblk - w + nb - 1) / nb; // blocks of this WG; 1 item per wave per block
+	auto addr = [&](int j) { return p + ((size_t)(j * nb + w) * 8 + v) * 1024 + lane * 16; };
+	const char *dummy = (const char *)vec + lane * 16;
+	u32x4 buf[U];
+	if (v != 0 || k == 0) {
+#pragma unroll
+		for (int u = 0; u < U; ++u)
+			buf[u] = ldnt(u < mine ? addr(u) : dummy);
+	}
+	if (k > 0) {
+		if (tid == 0) { // wave 0 has no loads queued ahead of its poll (in-order vmcnt)
+			long spins = 0;
+			// 8 replicas of each counter (128 B apart); poll this XCD's
+			while ((int)(ld_sc1u(counters + ((k - 1) * 8 + (w & 7)) * 32) - nb_prev) < 0) {
+				if (++spins > (1l << 22)) {
+					atomicCAS(err, 0u, 0x10000u + k);
+					break;
+				}
+				__builtin_amdgcn_s_sleep(SLEEP);
+			}
+		}
+		__syncthreads();
+		if (v == 0) {
+#pragma unroll
+			for (int u = 0; u < U; ++u)
+				buf[u] = ldnt(u < mine ? addr(u) : dummy);
+		}
+	}
+	for (int i = tid * 4; i < gather; i += 512 * 4)
+		*(f32x4 *)&xs[i] = ld_sc1x4(vec, i * 4);
+	__syncthreads();
+	unsigned acc = 0;
+	for (int kk = 0; kk < mine; kk += U) {
+#pragma unroll
+		for (int u = 0; u < U; ++u) {
+			const int j = kk + u;
+			if (j < mine)
+				acc ^= buf[u][0] ^ buf[u][1] ^ buf[u][2] ^ buf[u][3];
+			buf[u] = ldnt(j + U < mine ? addr(j + U) : dummy);
+		}
+	}
+	acc += __float_as_uint(xs[(tid * 7) % gather]);
+	if (tid < 16)
+		st_sc1f(vec + w * 16 + tid, (float)(acc & 0xff));
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	__syncthreads();
+	if (tid < 8) // one add per replica
+		__hip_atomic_fetch_add(counters + (k * 8 + tid) * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	if (acc == 0x12345678u)
+		out[0] = acc;
+}
+template <int SLEEP>
+__global__ __launch_bounds__(256) void chain_att_kernel(const char *kv, float *vec, int k, unsigned *counters,
+                                                        int nb_prev, unsigned *err) {
+	if (threadIdx.x == 0) {
+		long spins = 0;
+		while ((int)(ld_sc1u(counters + ((k - 1) * 8 + (blockIdx.x & 7)) * 32) - nb_prev) < 0) {
+			if (++spins > (1l << 22)) {
+				atomicCAS(err, 0u, 0x10000u + k);
+				break;
+			}
+			__builtin_amdgcn_s_sleep(SLEEP);
+		}
+	}
+	__syncthreads();
+	float s = 0.f;
+	const float *kb = (const float *)(kv + (size_t)blockIdx.x * ATT_BYTES);
+	for (int i = threadIdx.x * 4; i < ATT_BYTES / 4; i += 256 * 4) {
+		f32x4 t = ld_sc1x4(kb, i * 4);
+		s += t[0] + t[1] + t[2] + t[3];
+	}
+	if (threadIdx.x == 0)
+		st_sc1f(vec + blockIdx.x, s);
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	__syncthreads();
+	if (threadIdx.x < 8)
+		__hip_atomic_fetch_add(counters + (k * 8 + threadIdx.x) * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 int main(int argc, char **argv) {
 	setvbuf(stdout, NULL, _IONBF, 0);
 	const int L = 32;
@@ -447,6 +540,61 @@ int main(int argc, char **argv) {
 			}
 		});
 		report("launches (5 kernels/layer)", ms);
+	}
+	{
+		// same kernels, one stream, flags unused (k = 0 path) except the gather: reference for the chain
+		unsigned *cc, *cerr;
+		CHK(hipMalloc(&cc, 4 * 32 * 8 * 200));
+		CHK(hipMalloc(&cerr, 4));
+		CHK(hipMemset(cerr, 0, 4));
+		hipStream_t s2[2];
+		CHK(hipStreamCreateWithFlags(&s2[0], hipStreamNonBlocking));
+		CHK(hipStreamCreateWithFlags(&s2[1], hipStreamNonBlocking));
+		hipEvent_t ej;
+		CHK(hipEventCreateWithFlags(&ej, hipEventDisableTiming));
+		auto chain = [&](int nstreams, int SL) {
+			CHK(hipMemsetAsync(cc, 0, 4 * 32 * 8 * 200, 0));
+			CHK(hipEventRecord(ej, 0));
+			CHK(hipStreamWaitEvent(s2[0], ej, 0));
+			CHK(hipStreamWaitEvent(s2[1], ej, 0));
+			int k = 0, nb_prev = 0;
+			for (int l = 0; l < L; ++l) {
+				for (int p = 0; p < NPH; ++p) {
+					hipStream_t st = s2[nstreams == 2 ? (k & 1) : 0];
+					const int g = p == 3 ? 14336 : 4096;
+					if (SL == 1)
+						chain_kernel<4, 1><<<256, 512, 0, st>>>(w + l * layer + off[p], sz[p], k, cc, nb_prev, vec, g, cerr, out);
+					else
+						chain_kernel<4, 8><<<256, 512, 0, st>>>(w + l * layer + off[p], sz[p], k, cc, nb_prev, vec, g, cerr, out);
+					nb_prev = 256;
+					++k;
+					if (p == 0) {
+						st = s2[nstreams == 2 ? (k & 1) : 0];
+						if (SL == 1)
+							chain_att_kernel<1><<<ATT_WGS, 256, 0, st>>>(kv, vec, k, cc, nb_prev, cerr);
+						else
+							chain_att_kernel<8><<<ATT_WGS, 256, 0, st>>>(kv, vec, k, cc, nb_prev, cerr);
+						nb_prev = ATT_WGS;
+						++k;
+					}
+				}
+			}
+			CHK(hipEventRecord(ej, s2[0]));
+			CHK(hipStreamWaitEvent(0, ej, 0));
+			CHK(hipEventRecord(ej, s2[1]));
+			CHK(hipStreamWaitEvent(0, ej, 0));
+		};
+		for (int ns = 1; ns <= 2; ++ns)
+			for (int U : {1, 8}) {
+				float ms = timeit([&] { chain(ns, U); });
+				unsigned e;
+				CHK(hipMemcpy(&e, cerr, 4, hipMemcpyDeviceToHost));
+				char nm[96];
+				snprintf(nm, sizeof nm, "chain %d stream(s) sleep=%d%s", ns, U, e ? " SEAM TIMEOUT" : "");
+				report(nm, ms);
+				if (e)
+					exit(1);
+			}
 	}
 	Args a{};
 	a.base = w;

@@ -19,6 +19,10 @@
 
 #define GEMV_THREADS 256
 
+#ifdef YALM_WG_TRACE
+__device__ unsigned long long *yalm_wg_trace;
+#endif
+
 template <class WT, int R_>
 struct PStore {
 	static constexpr int R = R_;
@@ -424,6 +428,9 @@ __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__re
 	float *part = xs + ((n + 3) & ~3) + 64;                         // [ngl * R][W]
 	const size_t lane_off = (size_t)lane * EPL * WT::BYTES;
 	const char *dummy = (const char *)x + lane * 16;
+#ifdef YALM_WG_TRACE
+	const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+#endif
 
 	auto advance = [&](int &vr, int &c) {
 		c += W;
@@ -490,4 +497,10 @@ __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__re
 		}
 		p.finish_all(b + gl * NB, a);
 	}
+#ifdef YALM_WG_TRACE // tools/wg_timeline.hip: per-workgroup start/end (s_memrealtime, 100 MHz)
+	if (threadIdx.x == 0) {
+		yalm_wg_trace[2 * b] = t_start;
+		yalm_wg_trace[2 * b + 1] = __builtin_amdgcn_s_memrealtime();
+	}
+#endif
 }
