@@ -144,3 +144,20 @@ def test_synth_device_matches_host_bitwise():
         runtime.lib.yalm_free(p)
         ref = M.synth_array(n, dt, seed, scale, off).view(np.uint8)
         np.testing.assert_array_equal(host, ref)
+
+
+@pytest.mark.parametrize("n", [1024, 2064])
+def test_fp8_every_byte_exact(n):
+    """Every E5M2 byte value through the GEMV's fp8 unpack (v_cvt_pk_f32_bf8 on
+    the row-block path n % 1024 == 0, the ragged path otherwise): row r holds
+    byte r everywhere, x is one-hot, so out[r] must equal e5m2(r) exactly
+    (NaN bytes give NaN; inf * 0 gives NaN, as in the float64 twin)."""
+    w = np.repeat(np.arange(256, dtype=np.uint8)[:, None], n, axis=1)
+    x = np.zeros(n, np.float32)
+    x[n // 3] = 1.0
+    g = rt().matmul(x, w, M.F8E5M2)
+    ref = (M.e5m2_to_f32(w).astype(np.float64) * x.astype(np.float64)).sum(axis=1)
+    fin = np.isfinite(ref)
+    assert fin.sum() == 256 - 8  # 2 infinities + 6 NaNs -> non-finite sums
+    np.testing.assert_array_equal(g[fin], ref[fin].astype(np.float32))
+    assert np.all(np.isnan(g[~fin]))

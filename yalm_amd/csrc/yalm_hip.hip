@@ -235,14 +235,32 @@ static int launch_rb_t(const P &p, const float *x, const float *normw, float eps
 	return YALM_OK;
 }
 
-// Per-kind defaults from tools/sweep_gemv.py on MI355X (profiles/r1_sweep_rb.txt):
-// 512 threads and U = 4 everywhere; QKV 2 and logits 4 workgroups per CU.
+// Per-kind, per-weight-type defaults from tools/sweep_gemv.py on MI355X
+// (profiles/r1_sweep_rb*.txt): {threads, U, workgroups per CU}.
+template <class WT>
 static GemvCfg default_rb_cfg(int kind) {
-	if (kind == GK_QKV)
-		return GemvCfg{512, 4, 2};
-	if (kind == GK_CLS)
+	if constexpr (WT::BYTES == 1) { // fp8: more ALU per byte -> fewer loads in flight per lane
+		switch (kind) {
+		case GK_W2:
+			return GemvCfg{512, 4, 1};
+		case GK_GLU:
+			return GemvCfg{1024, 2, 2};
+		default:
+			return GemvCfg{512, 2, 2};
+		}
+	}
+	switch (kind) {
+	case GK_QKV:
+		return GemvCfg{512, 2, 2};
+	case GK_WO:
+		return GemvCfg{1024, 2, 2};
+	case GK_W2:
+		return GemvCfg{1024, 2, 1};
+	case GK_CLS:
 		return GemvCfg{512, 4, 4};
-	return GemvCfg{512, 4, 1};
+	default:
+		return GemvCfg{512, 4, 1};
+	}
 }
 
 template <class WT, class P, bool NORM, int THREADS>
@@ -260,7 +278,7 @@ static int launch_rb_u(const P &p, const float *x, const float *normw, float eps
 template <class WT, class P, bool NORM>
 static int launch_rb(const P &p, const float *x, const float *normw, float eps, int kind, GemvCfg want,
                      hipStream_t st) {
-	const GemvCfg def = default_rb_cfg(kind);
+	const GemvCfg def = default_rb_cfg<WT>(kind);
 	const int threads = want.threads ? want.threads : def.threads;
 	const int U = want.U ? want.U : def.U;
 	const int wpc = want.gpw ? want.gpw : def.gpw;
