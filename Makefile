@@ -4,13 +4,18 @@ CXX ?= g++
 ARCH ?= gfx950
 HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall
 CSRC = yalm_amd/csrc
-HIP_SRCS = $(CSRC)/yalm_hip.hip
+HIP_SRCS = $(CSRC)/yalm_hip.hip $(CSRC)/prefill.hip
+HIP_OBJS = $(patsubst $(CSRC)/%.hip,build/%.o,$(HIP_SRCS))
 HIP_HDRS = $(wildcard $(CSRC)/*.h) include/yalm_hip.h
 
 all: yalm_amd/libyalm_hip.so oracle host
 
-yalm_amd/libyalm_hip.so: $(HIP_SRCS) $(HIP_HDRS)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(HIP_SRCS)
+yalm_amd/libyalm_hip.so: $(HIP_OBJS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(HIP_OBJS)
+
+build/%.o: $(CSRC)/%.hip $(HIP_HDRS)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
 oracle:
 	$(MAKE) -C oracle
@@ -20,11 +25,11 @@ host: yalm_amd/libyalm_hip.so
 
 # kernel resource usage (VGPR/SGPR/LDS/occupancy) report
 resource-usage:
-	$(HIPCC) $(HIPFLAGS) -c -o /tmp/yalm_ru.o $(HIP_SRCS) -Rpass-analysis=kernel-resource-usage 2>&1 | \
+	for f in $(HIP_SRCS); do $(HIPCC) $(HIPFLAGS) -c -o /tmp/yalm_ru.o $$f -Rpass-analysis=kernel-resource-usage 2>&1; done | \
 		grep -E "Function Name|VGPRs:|SGPRs|Occupancy|LDS Size" | paste - - - - - -
 
 clean:
-	rm -f yalm_amd/libyalm_hip.so
+	rm -f yalm_amd/libyalm_hip.so $(HIP_OBJS)
 	$(MAKE) -C oracle clean
 	$(MAKE) -C yalm_amd/host clean
 

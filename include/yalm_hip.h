@@ -147,6 +147,26 @@ int yalm_set_gemv_config(yalm_decoder d, int kind, int threads, int unroll, int 
 /* Name of kernel_id's device function (to match rocprofv3 summaries). */
 const char *yalm_kernel_name(yalm_decoder d, int kernel_id);
 
+/* ---------------- batched prefill (MFMA): the perplexity / prompt path ----------------
+ * Replaces the reference's position-by-position forward loop over a prompt
+ * (main.cpp:128-200 `-m perplexity`, main.cpp:95-101 prompt hydration,
+ * Model::forward per position, model.cpp:396-407) with one pass per layer
+ * over all n positions: rmsnorm + QKV GEMM + RoPE + fp16 KV-cache write, causal
+ * GQA attention, Wo / W1|W3 / W2 GEMMs on the f16 MFMA units.
+ * Fills the KV cache rows pos0 .. pos0 + n - 1 exactly where the decoder
+ * expects them, so yalm_forward / yalm_generate_greedy can continue at
+ * pos0 + n. logprobs (host, n floats, may be NULL): logprobs[i] =
+ * log softmax(logits at position pos0 + i)[tokens[i + 1]] for i < n - 1 (the
+ * quantity main.cpp:155 sums), logprobs[n - 1] = 0. Requires f16 weights,
+ * dims multiple of 128, head_dim 64 | 128 and pos0 + n <= max_seq_len
+ * (the sliding window past max_seq_len stays on the decode path).
+ * Synchronous. Activations are rounded to f16 for the MFMA inputs: results
+ * match the decode path within the tolerance stated in tests/test_gpu_prefill.py. */
+int yalm_prefill(yalm_decoder d, const int *tokens, int n, int pos0, float *logprobs);
+/* Average device time (ms) of one n-position prefill with log-probs (synthetic
+ * token ids), over `iters` back-to-back runs (bench_prefill.py). */
+int yalm_prefill_time(yalm_decoder d, int n, int iters, float *avg_ms);
+
 /* ---------------- test API: replaces infer.cu:890-1019 (model.h:370-384) ---------------- */
 /* Host pointers in and out; synchronous. dtype selects the weight type
  * (matmul_cuda<float|half|uint8_t>). */
@@ -158,6 +178,15 @@ int yalm_mha(float *xout, float *att, const uint16_t *kb, const uint16_t *vb, co
 /* ffn_cuda: xout = W2 (act(W1 x) * W3 x). */
 int yalm_ffn(float *xout, const float *x, const void *w1, const void *w2, const void *w3, int hidden_dim, int dim,
              int act, int dtype);
+
+/* Prefill building blocks (host pointers, synchronous):
+ * c[M][N] f32 = a[M][K] f16 · w[N][K]^T f16 (the MFMA GEMM; N % 128 == 0, K % 64 == 0). */
+int yalm_gemm_f16(float *c, const uint16_t *a, const uint16_t *w, int M, int N, int K);
+/* Causal GQA attention of T query rows at positions pos0 .. pos0 + T - 1:
+ * q [T][n_heads * head_dim] f16, kc / vc [pos0 + T][n_kv_heads * head_dim] f16,
+ * o [T][n_heads * head_dim] f16 (infer.cpp:216-248 per row and head). */
+int yalm_attn_prefill(uint16_t *o, const uint16_t *q, const uint16_t *kc, const uint16_t *vc, int T, int pos0,
+                      int n_heads, int n_kv_heads, int head_dim);
 
 #ifdef __cplusplus
 }

@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def declared_symbols():
     src = open(os.path.join(ROOT, "include", "yalm_hip.h")).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(yalm_[a-z_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(yalm_[a-z0-9_]+)\s*\(", src)))
 
 
 def test_header_declares_expected_entry_points():

@@ -1,0 +1,124 @@
+"""GPU parity of the batched MFMA prefill path (include/yalm_hip.h "batched
+prefill"): the GEMM and the causal attention against float64 numpy, and the
+whole prefill against the decode engine (itself pinned to the CPU oracle by
+test_gpu_decode.py), position by position.
+
+Tolerances: the prefill rounds activations to f16 for the MFMA inputs (A
+operands: normalised x, attention output, GLU output; P in attention), where
+the reference keeps them f32 (infer.cpp). The GEMM itself accumulates in f32,
+so on f16-exact inputs it is exact (test_gemm_exact_integers).
+  * log p(next token): |prefill - decode| <= LP_ATOL (nats)
+  * attention output: |o - o64| <= 4e-3 * max|v| + f16 rounding of o
+"""
+import numpy as np
+import pytest
+
+from yalm_amd import models as M
+
+pytestmark = pytest.mark.gpu
+
+LP_ATOL = 0.02  # nats, per position
+
+
+def rt():
+    from yalm_amd import runtime
+
+    return runtime
+
+
+@pytest.mark.parametrize("M_,N,K", [(128, 128, 64), (200, 256, 192), (37, 384, 128), (1, 128, 64)])
+def test_gemm_exact_integers(M_, N, K):
+    """Small asymmetric integers: every product and partial sum is exact in f32,
+    so the MFMA GEMM (fragment maps, LDS swizzle, M tail) must match exactly."""
+    rng = np.random.default_rng(M_ * N + K)
+    a = rng.integers(-4, 5, size=(M_, K)).astype(np.float16)
+    w = rng.integers(-4, 5, size=(N, K)).astype(np.float16)
+    w[:, 0] += np.arange(N, dtype=np.float16) % 7  # break row/column symmetry
+    c = rt().gemm_f16(a, w)
+    ref = a.astype(np.int64) @ w.astype(np.int64).T
+    np.testing.assert_array_equal(c, ref.astype(np.float32))
+
+
+@pytest.mark.parametrize("M_,N,K", [(300, 384, 512), (4096, 128, 3072)])
+def test_gemm_random(M_, N, K):
+    rng = np.random.default_rng(7)
+    a = rng.standard_normal((M_, K)).astype(np.float16)
+    w = (rng.standard_normal((N, K)) * 0.02).astype(np.float16)
+    c = rt().gemm_f16(a, w)
+    ref = a.astype(np.float64) @ w.astype(np.float64).T
+    err = np.max(np.abs(c - ref)) / np.max(np.abs(ref))
+    assert err < 1e-5, err
+
+
+def _attn_ref(q, kc, vc, T, pos0, nh, nkv, D):
+    q = q.astype(np.float64).reshape(T, nh, D)
+    k = kc.astype(np.float64).reshape(-1, nkv, D)
+    v = vc.astype(np.float64).reshape(-1, nkv, D)
+    out = np.zeros((T, nh, D))
+    G = nh // nkv
+    for t in range(T):
+        n = pos0 + t + 1
+        for h in range(nh):
+            s = k[:n, h // G] @ q[t, h] / np.sqrt(D)
+            p = np.exp(s - s.max())
+            p /= p.sum()
+            out[t, h] = p @ v[:n, h // G]
+    return out.reshape(T, nh * D)
+
+
+@pytest.mark.parametrize("T,pos0", [(1, 0), (37, 0), (128, 0), (200, 0), (70, 50)])
+@pytest.mark.parametrize("nh,nkv,D", [(8, 2, 64), (4, 4, 128), (6, 2, 128)])
+def test_attn_prefill(T, pos0, nh, nkv, D):
+    rng = np.random.default_rng(T * 31 + pos0 + D)
+    q = rng.standard_normal((T, nh * D)).astype(np.float16)
+    kc = rng.standard_normal((pos0 + T, nkv * D)).astype(np.float16)
+    vc = rng.standard_normal((pos0 + T, nkv * D)).astype(np.float16)
+    o = rt().attn_prefill(q, kc, vc, T, pos0, nh, nkv, D).astype(np.float64)
+    ref = _attn_ref(q, kc, vc, T, pos0, nh, nkv, D)
+    np.testing.assert_allclose(o, ref, atol=4e-3 * np.abs(vc).max(), rtol=2e-3)
+
+
+def _decode_logprobs(dec, tokens):
+    lp = []
+    for pos, t in enumerate(tokens[:-1]):
+        logits = dec.forward(int(t), pos).astype(np.float64)
+        m = logits.max()
+        lp.append(logits[tokens[pos + 1]] - m - np.log(np.exp(logits - m).sum()))
+    return np.array(lp)
+
+
+CFGS = {
+    "small-d64": M.SMALL,
+    "gqa-d128": M.ModelConfig(dim=512, hidden_dim=1024, head_dim=128, n_layers=3, n_heads=4, n_kv_heads=2,
+                              vocab_size=1024, max_seq_len=320, rope_theta=1e6, act=M.SILU, weight_dtype=M.F16),
+}
+
+
+@pytest.mark.parametrize("name", list(CFGS))
+@pytest.mark.parametrize("n", [1, 61, 200])
+def test_prefill_matches_decode(name, n):
+    """Per-position log p(next) of one prefill pass vs the decode engine run
+    position by position (the reference's perplexity loop), same weights."""
+    cfg = CFGS[name]
+    R = rt()
+    dm = R.DeviceModel.synthetic(cfg, seed=3)
+    rng = np.random.default_rng(n)
+    tokens = rng.integers(0, cfg.vocab_size, size=n).astype(np.int32)
+    dec_p = R.Decoder(dm)
+    lp_p = dec_p.prefill(tokens)
+    dec_d = R.Decoder(dm)
+    lp_d = _decode_logprobs(dec_d, tokens)
+    err = np.max(np.abs(lp_p[: n - 1] - lp_d)) if n > 1 else 0.0
+    assert lp_p[n - 1] == 0.0
+    assert err <= LP_ATOL, (name, n, err)
+    # the KV cache the prefill wrote drives the decoder: the next step's logits agree
+    nxt = int(rng.integers(0, cfg.vocab_size))
+    if n < cfg.max_seq_len:
+        lg_p = dec_p.forward(nxt, n)
+        lg_d = dec_d.forward(int(tokens[-1]), n - 1) if n > 0 else None
+        lg_d = dec_d.forward(nxt, n)
+        rel = np.max(np.abs(lg_p - lg_d)) / np.max(np.abs(lg_d))
+        assert rel < 5e-3, rel
+    dec_p.close()
+    dec_d.close()
+    dm.close()

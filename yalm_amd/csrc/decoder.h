@@ -1,0 +1,92 @@
+// decoder.h — host-side state shared by the engine's translation units
+// (yalm_hip.hip: shim, decoder, decode test API; prefill.hip: batched prefill).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/yalm_hip.h"
+#include "device_common.h"
+
+// ------------------------------------------------------------------ errors
+void set_err(const std::string &s); // yalm_hip.hip (thread-local last error)
+
+#define HIPCHK(expr)                                                                                                   \
+	do {                                                                                                               \
+		hipError_t e_ = (expr);                                                                                        \
+		if (e_ != hipSuccess) {                                                                                        \
+			set_err(std::string(#expr) + " failed: " + hipGetErrorString(e_) + " (" + __FILE__ + ":" +                 \
+			        std::to_string(__LINE__) + ")");                                                                   \
+			return YALM_ERR_HIP;                                                                                       \
+		}                                                                                                              \
+	} while (0)
+
+#define ARGCHK(cond, msg)                                                                                              \
+	do {                                                                                                               \
+		if (!(cond)) {                                                                                                 \
+			set_err(msg);                                                                                              \
+			return YALM_ERR_ARG;                                                                                       \
+		}                                                                                                              \
+	} while (0)
+
+#define TRY(expr)                                                                                                      \
+	do {                                                                                                               \
+		int r_ = (expr);                                                                                               \
+		if (r_ != YALM_OK)                                                                                             \
+			return r_;                                                                                                 \
+	} while (0)
+
+// GEMV launch geometry (see gemv_stream_kernel). 0 = automatic.
+struct GemvCfg {
+	int threads = 0, U = 0, gpw = 0;
+};
+enum { GK_QKV = 0, GK_WO = 1, GK_GLU = 2, GK_W2 = 3, GK_CLS = 4, GK_N = 5 };
+
+int device_cu_count();
+
+// Batched-prefill scratch (prefill.hip), allocated on first use for
+// max_seq_len rows.
+struct PrefillBufs {
+	int cap = 0;
+	float *X = nullptr;        // [cap][dim] f32 residual stream
+	uint16_t *Xn = nullptr;    // [cap][dim] f16 normalised A operand
+	uint16_t *Q = nullptr;     // [cap][q_dim] f16
+	uint16_t *O = nullptr;     // [cap][q_dim] f16 attention output
+	uint16_t *H = nullptr;     // [cap][hidden] f16 GLU output
+	int *tok = nullptr;        // [cap] token ids
+	int *tgt = nullptr;        // [cap] next-token targets (-1: none)
+	float *pmax = nullptr, *psum = nullptr; // [cap][vocab / 128] logits partials
+	float *tgt_logit = nullptr, *lp = nullptr; // [cap]
+};
+
+// ------------------------------------------------------------------ decoder
+enum { GRAPH_HYDRATE = 0, GRAPH_LOGITS = 1, GRAPH_GREEDY = 2, N_GRAPHS = 3 };
+
+struct yalm_decoder_s {
+	yalm_config c{};
+	std::vector<yalm_block_weights> b;
+	const void *emb = nullptr;
+	const float *rms_final = nullptr;
+	const void *wcls = nullptr;
+	hipStream_t stream = nullptr;
+	bool own_stream = false;
+	StepState *step = nullptr;
+	float *x = nullptr, *q = nullptr, *xb2 = nullptr, *hb = nullptr, *part = nullptr, *logits = nullptr,
+	      *inv_freq = nullptr;
+	int *tokens = nullptr;
+	int tokens_cap = 0;
+	float *logits_pinned = nullptr;
+	std::vector<void *> dev_allocs;
+	hipGraph_t graph[N_GRAPHS] = {};
+	hipGraphExec_t exec[N_GRAPHS] = {};
+	unsigned *attn_counters = nullptr; // per-kv-head arrival tickets (zeroed; the last arriver resets)
+	GemvCfg gemv[GK_N];
+	bool eager = false;     // YALM_EAGER=1: launch kernels directly (profilers that mis-handle graph replay)
+	bool graph_sync = false; // YALM_GRAPH_SYNC=1: synchronise after every replay
+	int ablate = 0;          // YALM_ABLATE bitmask: skip qkv|attn|wo|glu|w2 (1|2|4|8|16), timing only
+	std::string kname;
+	PrefillBufs pf;
+};
+

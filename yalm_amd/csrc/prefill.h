@@ -1,0 +1,568 @@
+// prefill.h — batched prefill / perplexity path on the matrix cores (MFMA).
+//
+// The reference has no batched prefill: `-m perplexity` (main.cpp:128-200)
+// and prompt hydration run the single-token forward once per position. Here
+// the T positions of a prompt go through each layer together, so every weight
+// matrix is read once per prompt instead of once per token and the work is
+// dense GEMMs on the gfx950 MFMA units:
+//   X[T, dim] f32 residual stream (infer.cpp:443-523 semantics per row)
+//   Xn = f16(rmsnorm(X) * w)                         (A operand of the GEMMs)
+//   [Q | K | V] = Xn · [Wq | Wk | Wv]^T   + clip + RoPE; K, V -> the fp16 cache
+//   O = causal GQA attention(Q, Kcache, Vcache)      (flash-style, MFMA)
+//   X += O · Wo^T
+//   H = f16(silu(Xn · W1^T) * (Xn · W3^T))           (one GEMM, two B operands)
+//   X += H · W2^T
+//   logits = f16(rmsnorm(X)) · Wcls^T -> per-row (max, sum exp, target logit)
+// Weights stay in the .yalm layout ([out][in] f16, row-major): C = A · W^T is
+// an "NT" GEMM whose two operands are both K-contiguous, so every MFMA operand
+// fragment is a 16-byte row read (no transposes). Accumulation is f32; the
+// activations are rounded to f16 for the MFMA inputs (the parity tolerance of
+// tests/test_gpu_prefill.py covers exactly that).
+#pragma once
+
+#include <float.h>
+
+#include "device_common.h"
+
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+#define YALM_LDS __attribute__((address_space(3)))
+
+namespace pf {
+
+constexpr int BM = 128, BN = 128, BK = 64; // block tile; BK = 64 f16 = 128-byte rows
+constexpr int THREADS = 256;               // 4 waves as 2 (M) x 2 (N), 64 x 64 each
+constexpr int TILE = BM * BK;              // f16 elements per staged operand tile (16 KB)
+
+__device__ __forceinline__ uint16_t f2h_bits(float x) {
+	_Float16 h = (_Float16)x;
+	uint16_t u;
+	__builtin_memcpy(&u, &h, 2);
+	return u;
+}
+
+// Stage a 128-row x 64-k f16 tile global -> LDS with 16-byte LDS-DMA
+// (global_load_lds_dwordx4): wave-instruction = 1 KB = 8 rows. The LDS image
+// is lane-linear; the XOR swizzle (chunk ^ (row & 7)) goes on the per-lane
+// SOURCE address, the matching read is frag_addr below. Rows past `rows`
+// re-read the last valid row (never stored).
+__device__ __forceinline__ void stage_tile(uint16_t *lds_tile, const uint16_t *__restrict__ g, int ld, int row0,
+                                           int rows, int k0, int wave, int lane) {
+#pragma unroll
+	for (int i = 0; i < BM / 8 / (THREADS / 64); ++i) {
+		const int rb = wave * (BM / 8 / (THREADS / 64)) + i;
+		const int r = rb * 8 + (lane >> 3);
+		const int c = lane & 7;
+		const int gr = min(row0 + r, rows - 1);
+		const uint16_t *src = g + (size_t)gr * ld + k0 + 8 * (c ^ (r & 7));
+		__builtin_amdgcn_global_load_lds((const void *)src, (YALM_LDS void *)(lds_tile + rb * 8 * BK), 16, 0, 0);
+	}
+}
+
+// 32x32x16 f16 operand fragment of tile row r, k-step s (16 deep): lane half h
+// holds k = 16 s + 8 h .. +7 (cdna_hip_programming.md §3 A/B lane maps).
+__device__ __forceinline__ half8_t frag(const uint16_t *lds_tile, int r, int s, int h) {
+	const int kc = 2 * s + h;
+	return *(const half8_t *)(lds_tile + r * BK + 8 * (kc ^ (r & 7)));
+}
+
+// C/D map of v_mfma_f32_32x32x16: column = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5).
+__device__ __forceinline__ int crow(int reg, int lane) { return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); }
+
+// ---------------------------------------------------------------- epilogues
+// Each gets the wave's accumulators acc[NB][2][2] (32x32 tiles, rows m0 + 32 i,
+// columns n0 + 32 j) after the K loop.
+
+struct EpiStoreF32 { // C -> f32 (tests)
+	static constexpr bool NEEDS_LDS = false;
+	float *red = nullptr;
+	float *c;
+	int ldc, M;
+	template <int NB>
+	__device__ __forceinline__ void apply(f32x16_t (&acc)[NB][2][2], int m0, int n0, int lane) const {
+#pragma unroll
+		for (int i = 0; i < 2; ++i)
+#pragma unroll
+			for (int j = 0; j < 2; ++j)
+#pragma unroll
+				for (int r = 0; r < 16; ++r) {
+					const int m = m0 + 32 * i + crow(r, lane), n = n0 + 32 * j + (lane & 31);
+					if (m < M)
+						c[(size_t)m * ldc + n] = acc[0][i][j][r];
+				}
+	}
+};
+
+struct EpiResidual { // X[m][n] += C  (fused_matmul_add_residuals, per row)
+	static constexpr bool NEEDS_LDS = false;
+	float *red = nullptr;
+	float *x;
+	int ldx, M;
+	template <int NB>
+	__device__ __forceinline__ void apply(f32x16_t (&acc)[NB][2][2], int m0, int n0, int lane) const {
+#pragma unroll
+		for (int i = 0; i < 2; ++i)
+#pragma unroll
+			for (int j = 0; j < 2; ++j)
+#pragma unroll
+				for (int r = 0; r < 16; ++r) {
+					const int m = m0 + 32 * i + crow(r, lane), n = n0 + 32 * j + (lane & 31);
+					if (m < M)
+						x[(size_t)m * ldx + n] += acc[0][i][j][r];
+				}
+	}
+};
+
+template <int ACT>
+struct EpiGlu { // H = f16(act(X W1^T) * (X W3^T))  (fused_ffn_w1_w3_glu_act)
+	static constexpr bool NEEDS_LDS = false;
+	float *red = nullptr;
+	uint16_t *h;
+	int ldh, M;
+	template <int NB>
+	__device__ __forceinline__ void apply(f32x16_t (&acc)[NB][2][2], int m0, int n0, int lane) const {
+#pragma unroll
+		for (int i = 0; i < 2; ++i)
+#pragma unroll
+			for (int j = 0; j < 2; ++j)
+#pragma unroll
+				for (int r = 0; r < 16; ++r) {
+					const int m = m0 + 32 * i + crow(r, lane), n = n0 + 32 * j + (lane & 31);
+					if (m < M)
+						h[(size_t)m * ldh + n] = f2h_bits(act_fn<ACT>(acc[0][i][j][r]) * acc[NB - 1][i][j][r]);
+				}
+	}
+};
+
+// [q | k | v] columns: clip (infer.cpp:280-288), RoPE on (even, odd) column
+// pairs = lanes (l, l ^ 1) via DPP (infer.cpp:291-301, angle = pos * freq),
+// q -> f16 Q[T][q_dim], k / v -> the fp16 KV cache rows pos0 + m
+// (fused_rope_and_cache_update, infer.cu:642-677).
+struct EpiQKV {
+	static constexpr bool NEEDS_LDS = false;
+	float *red = nullptr;
+	uint16_t *q;
+	uint16_t *kc, *vc;
+	const float *inv_freq;
+	int M, q_dim, kv_dim, head_dim, pos0;
+	float clip;
+	template <int NB>
+	__device__ __forceinline__ void apply(f32x16_t (&acc)[NB][2][2], int m0, int n0, int lane) const {
+		const bool odd = lane & 1;
+#pragma unroll
+		for (int i = 0; i < 2; ++i)
+#pragma unroll
+			for (int j = 0; j < 2; ++j) {
+				const int n = n0 + 32 * j + (lane & 31);
+				const bool is_v = n >= q_dim + kv_dim;
+				const int nn = n < q_dim ? n : (n < q_dim + kv_dim ? n - q_dim : n - q_dim - kv_dim);
+				const float freq = inv_freq[(nn % head_dim) >> 1];
+#pragma unroll
+				for (int r = 0; r < 16; ++r) {
+					float v = acc[0][i][j][r];
+					v = v < -clip ? -clip : (v > clip ? clip : v);
+					const float p = dpp<0xB1>(v); // partner column (n ^ 1)
+					const int m = m0 + 32 * i + crow(r, lane);
+					if (m >= M)
+						continue;
+					const int pos = pos0 + m;
+					float o = v;
+					if (!is_v) {
+						const float val = (float)pos * freq;
+						const float fcr = cosf(val), fci = sinf(val);
+						o = odd ? p * fci + v * fcr : v * fcr - p * fci;
+					}
+					if (n < q_dim)
+						q[(size_t)m * q_dim + n] = f2h_bits(o);
+					else if (!is_v)
+						kc[(size_t)pos * kv_dim + nn] = f2h(o);
+					else
+						vc[(size_t)pos * kv_dim + nn] = f2h(o);
+				}
+			}
+	}
+};
+
+// Per (row, 128-column tile): max and sum of exp over the tile's logits, and
+// the target token's logit when it falls in the tile (sample_prob,
+// sampler.cpp:11-25, split over vocab tiles; combined by logprob_kernel).
+struct EpiLogits {
+	static constexpr bool NEEDS_LDS = true;
+	float *pmax, *psum, *tgt_logit;
+	const int *targets; // target token of row m (-1: none)
+	int M, ntiles;
+	float *red; // LDS scratch [2 waves (N)][128 rows][2]
+	template <int NB>
+	__device__ __forceinline__ void apply(f32x16_t (&acc)[NB][2][2], int m0, int n0, int lane) const {
+		const int wave = threadIdx.x >> 6;
+		const int wn = wave & 1, wm = wave >> 1;
+#pragma unroll
+		for (int i = 0; i < 2; ++i) {
+#pragma unroll
+			for (int r = 0; r < 16; ++r) {
+				const int ml = 32 * i + crow(r, lane); // row within the wave's 64
+				const int m = m0 + ml;
+				const int tgt = m < M ? targets[m] : -1;
+				float mx = fmaxf(acc[0][i][0][r], acc[0][i][1][r]);
+				mx = row16_max(mx);
+				mx = fmaxf(mx, xor16(mx)); // 32 columns of this lane half
+#pragma unroll
+				for (int j = 0; j < 2; ++j) {
+					const int n = n0 + 32 * j + (lane & 31);
+					if (n == tgt)
+						tgt_logit[m] = acc[0][i][j][r];
+				}
+				float s = expf(acc[0][i][0][r] - mx) + expf(acc[0][i][1][r] - mx);
+				s = row16_sum(s);
+				s += xor16(s);
+				if ((lane & 31) == 0) {
+					red[(wn * BM + wm * 64 + ml) * 2 + 0] = mx;
+					red[(wn * BM + wm * 64 + ml) * 2 + 1] = s;
+				}
+			}
+		}
+		__syncthreads();
+		for (int row = threadIdx.x; row < BM; row += THREADS) {
+			const int m = m0 - (m0 % BM) + row; // block's row
+			if (m >= M)
+				continue;
+			const float a = red[row * 2], sa = red[row * 2 + 1];
+			const float b = red[(BM + row) * 2], sb = red[(BM + row) * 2 + 1];
+			const float mx = fmaxf(a, b);
+			const int tile = (n0 - (n0 % BN)) / BN;
+			pmax[(size_t)m * ntiles + tile] = mx;
+			psum[(size_t)m * ntiles + tile] = sa * expf(a - mx) + sb * expf(b - mx);
+		}
+	}
+};
+
+// B operand rows n = 0..N-1 drawn from up to 3 row-major [rows][K] matrices
+// laid end to end (wq | wk | wv). Every 128-row tile lies inside one segment.
+struct BSrc {
+	const uint16_t *p[3];
+	int end[3]; // exclusive row end of each segment (cumulative)
+	__device__ __forceinline__ void tile(int col0, const uint16_t *&base, int &r0, int &rows) const {
+		int s = col0 < end[0] ? 0 : (col0 < end[1] ? 1 : 2);
+		const int start = s == 0 ? 0 : end[s - 1];
+		base = p[s];
+		r0 = col0 - start;
+		rows = end[s] - start;
+	}
+};
+
+// C[M, N] (epilogue) = A[M, K] · W_b[N, K]^T for b < NB (NB = 2: W1 and W3
+// share the A tile). N % 128 == 0, K % 64 == 0, any M. Two LDS buffers; the
+// next K tile's LDS-DMA is issued before the current tile's MFMAs (the
+// 2-phase structure of cdna_hip_programming.md §5.5 T3+T4, minimum form).
+template <class EPI, int NB>
+__global__ __launch_bounds__(THREADS) void gemm_nt_kernel(const uint16_t *__restrict__ A, int M, int K, BSrc B0,
+                                                          BSrc B1, int N, EPI epi) {
+	extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+	constexpr int BUF = (1 + NB) * TILE; // f16 per buffer
+	const int lane = threadIdx.x & 63;
+	const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	const int wm = wave >> 1, wn = wave & 1;
+	const int h = lane >> 5, l32 = lane & 31;
+
+	// tile index: XCD-aware (blocks b, b+8, ... share an XCD's L2): consecutive
+	// tiles of one XCD walk down M for a fixed N panel (the W panel is reused)
+	const int tiles_m = (M + BM - 1) / BM, tiles_n = N / BN;
+	const int nwg = tiles_m * tiles_n;
+	int wg = blockIdx.x;
+	{
+		const int q = nwg / 8, rr = nwg % 8, xcd = wg % 8, idx = wg / 8;
+		wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
+	}
+	const int tm = wg % tiles_m, tn = wg / tiles_m;
+	const int row0 = tm * BM, col0 = tn * BN;
+
+	f32x16_t acc[NB][2][2];
+#pragma unroll
+	for (int b = 0; b < NB; ++b)
+#pragma unroll
+		for (int i = 0; i < 2; ++i)
+#pragma unroll
+			for (int j = 0; j < 2; ++j)
+				acc[b][i][j] = f32x16_t{};
+
+	const int nk = K / BK;
+	const uint16_t *w0, *w1 = nullptr;
+	int w0r, w0n, w1r = 0, w1n = 1;
+	B0.tile(col0, w0, w0r, w0n);
+	if constexpr (NB == 2)
+		B1.tile(col0, w1, w1r, w1n);
+	auto stage = [&](int buf, int kt) {
+		uint16_t *base = smem + buf * BUF;
+		stage_tile(base, A, K, row0, M, kt * BK, wave, lane);
+		stage_tile(base + TILE, w0, K, w0r, w0n, kt * BK, wave, lane);
+		if constexpr (NB == 2)
+			stage_tile(base + 2 * TILE, w1, K, w1r, w1n, kt * BK, wave, lane);
+	};
+	stage(0, 0);
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	__syncthreads();
+	int cur = 0;
+	for (int kt = 0; kt < nk; ++kt) {
+		if (kt + 1 < nk)
+			stage(cur ^ 1, kt + 1);
+		const uint16_t *a_t = smem + cur * BUF;
+#pragma unroll
+		for (int s = 0; s < BK / 16; ++s) {
+			half8_t af[2], bf[NB][2];
+#pragma unroll
+			for (int i = 0; i < 2; ++i)
+				af[i] = frag(a_t, wm * 64 + 32 * i + l32, s, h);
+#pragma unroll
+			for (int b = 0; b < NB; ++b)
+#pragma unroll
+				for (int j = 0; j < 2; ++j)
+					bf[b][j] = frag(a_t + (1 + b) * TILE, wn * 64 + 32 * j + l32, s, h);
+#pragma unroll
+			for (int b = 0; b < NB; ++b)
+#pragma unroll
+				for (int i = 0; i < 2; ++i)
+#pragma unroll
+					for (int j = 0; j < 2; ++j)
+						acc[b][i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[b][j], acc[b][i][j], 0, 0, 0);
+		}
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		__syncthreads();
+		cur ^= 1;
+	}
+	EPI e = epi;
+	if constexpr (EPI::NEEDS_LDS)
+		e.red = (float *)smem; // the staging buffers are free after the K loop's last barrier
+	e.template apply<NB>(acc, row0 + wm * 64, col0 + wn * 64, lane);
+}
+
+// ---------------------------------------------------------------- attention
+// Causal GQA attention for the prompt rows (flash-style, online softmax),
+// infer.cpp:216-248 per (position, head): s_t = q·k_t / sqrt(D) over keys
+// t <= pos, softmax, o = sum_t p_t v_t. Keys/values come from the fp16 cache
+// rows 0 .. pos0 + T - 1 (written by the QKV epilogue). Grid (query blocks of
+// 128, q heads), 4 waves x 32 queries. Per 64-key tile:
+//   S = Q K^T   (A = Q fragments kept in registers, B = K rows from LDS)
+//   online softmax in the C layout (key on the lane: row reductions are
+//   DPP/permlane over 32 lanes, rows = registers)
+//   O += P V    (P via a per-wave LDS transpose; V staged transposed in LDS so
+//   its B fragments are row reads)
+constexpr int AQ = 128, AKT = 64; // queries per workgroup, keys per tile
+
+template <int D>
+__global__ __launch_bounds__(THREADS) void attn_prefill_kernel(const uint16_t *__restrict__ Q,
+                                                               const uint16_t *__restrict__ kc,
+                                                               const uint16_t *__restrict__ vc, int T, int pos0,
+                                                               int n_heads, int n_kv, uint16_t *__restrict__ O) {
+	static_assert(D % 16 == 0 && D <= 256, "head_dim");
+	constexpr int DCH = D / 8;                   // 16-byte chunks per K row
+	__shared__ __attribute__((aligned(16))) uint16_t Ks[AKT * D]; // [key][D], chunk ^ (key % DCH)
+	__shared__ __attribute__((aligned(16))) uint16_t Vt[D * AKT]; // [d][key], chunk ^ (d & 7)
+	__shared__ __attribute__((aligned(16))) uint16_t Ps[4][32 * AKT]; // per wave [query][key]
+	const int lane = threadIdx.x & 63, l32 = lane & 31, hh = lane >> 5;
+	const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	const int qb = gridDim.x - 1 - blockIdx.x; // heaviest (latest) query blocks first
+	const int h = blockIdx.y, g = h / (n_heads / n_kv);
+	const int q_dim = n_heads * D, kv_dim = n_kv * D;
+	const int qw0 = qb * AQ + wave * 32; // this wave's first query row
+	const float scale = 1.0f / sqrtf((float)D);
+	const int kv_rows = pos0 + T; // valid cache rows (masked keys past a query are never used)
+
+	half8_t qf[D / 16];
+	{
+		const uint16_t *qp = Q + (size_t)min(qw0 + l32, T - 1) * q_dim + h * D + 8 * hh;
+#pragma unroll
+		for (int s = 0; s < D / 16; ++s)
+			qf[s] = *(const half8_t *)(qp + 16 * s);
+	}
+	f32x16_t o[D / 32];
+#pragma unroll
+	for (int jd = 0; jd < D / 32; ++jd)
+		o[jd] = f32x16_t{};
+	float m_r[16], l_r[16];
+#pragma unroll
+	for (int r = 0; r < 16; ++r) {
+		m_r[r] = -FLT_MAX;
+		l_r[r] = 0.0f;
+	}
+	const int qmax_blk = min(qb * AQ + AQ, T) - 1;  // last query row of the block
+	const int ntile = (pos0 + qmax_blk) / AKT + 1;  // key tiles up to its position
+	uint16_t *ps = Ps[wave];
+
+	for (int kt = 0; kt < ntile; ++kt) {
+		const int key0 = kt * AKT;
+		// ---- stage K (LDS-DMA, lane-linear rows, swizzle on the source) and V^T (registers)
+		{
+			constexpr int ROWS_PER_INSTR = 1024 / (D * 2);
+#pragma unroll
+			for (int i = 0; i < AKT / ROWS_PER_INSTR / 4; ++i) {
+				const int rb = wave * (AKT / ROWS_PER_INSTR / 4) + i;
+				const int r = rb * ROWS_PER_INSTR + lane / DCH;
+				const int c = lane % DCH;
+				const uint16_t *src = kc + (size_t)min(key0 + r, kv_rows - 1) * kv_dim + g * D + 8 * (c ^ (r % DCH));
+				__builtin_amdgcn_global_load_lds((const void *)src, (YALM_LDS void *)(Ks + rb * ROWS_PER_INSTR * D), 16,
+				                                 0, 0);
+			}
+			// V^T: thread -> (key, 32-dim slab); 4 x 16-byte loads, 32 transposed 2-byte LDS writes
+			constexpr int SLABS = D / 32;
+			for (int e = threadIdx.x; e < AKT * SLABS; e += THREADS) {
+				const int key = e / SLABS, d0 = (e % SLABS) * 32;
+				const uint16_t *src = vc + (size_t)min(key0 + key, kv_rows - 1) * kv_dim + g * D + d0;
+#pragma unroll
+				for (int c = 0; c < 4; ++c) {
+					const u32x4_t v = load16(src + 8 * c);
+#pragma unroll
+					for (int w = 0; w < 4; ++w) {
+						const uint32_t pair = v[w];
+#pragma unroll
+						for (int half = 0; half < 2; ++half) {
+							const int d = d0 + 8 * c + 2 * w + half;
+							Vt[d * AKT + 8 * ((key >> 3) ^ (d & 7)) + (key & 7)] = (uint16_t)(pair >> (16 * half));
+						}
+					}
+				}
+			}
+		}
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		__syncthreads();
+
+		// ---- S = Q K^T for this wave's 32 queries x 64 keys
+		f32x16_t sacc[2];
+#pragma unroll
+		for (int j = 0; j < 2; ++j) {
+			sacc[j] = f32x16_t{};
+			const int kr = 32 * j + l32;
+#pragma unroll
+			for (int s = 0; s < D / 16; ++s) {
+				const int kcnk = 2 * s + hh;
+				const half8_t kb = *(const half8_t *)(Ks + kr * D + 8 * (kcnk ^ (kr % DCH)));
+				sacc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(qf[s], kb, sacc[j], 0, 0, 0);
+			}
+		}
+		// ---- online softmax; row (query) of register r: qw0 + crow(r, lane); key column: key0 + 32 j + l32
+#pragma unroll
+		for (int r = 0; r < 16; ++r) {
+			const int qpos = pos0 + qw0 + crow(r, lane);
+			float s0 = sacc[0][r] * scale, s1 = sacc[1][r] * scale;
+			if (key0 + l32 > qpos)
+				s0 = -FLT_MAX;
+			if (key0 + 32 + l32 > qpos)
+				s1 = -FLT_MAX;
+			float mx = fmaxf(s0, s1);
+			mx = row16_max(mx);
+			mx = fmaxf(mx, xor16(mx));
+			const float mn = fmaxf(m_r[r], mx);
+			const float alpha = expf(m_r[r] - mn);
+			const float p0 = expf(s0 - mn), p1 = expf(s1 - mn);
+			float ls = p0 + p1;
+			ls = row16_sum(ls);
+			ls += xor16(ls);
+			l_r[r] = l_r[r] * alpha + ls;
+			m_r[r] = mn;
+#pragma unroll
+			for (int jd = 0; jd < D / 32; ++jd)
+				o[jd][r] *= alpha;
+			const int qr = crow(r, lane); // P^T -> Ps[query][key]
+			ps[qr * AKT + 8 * ((l32 >> 3) ^ (qr & 7)) + (l32 & 7)] = f2h_bits(p0);
+			ps[qr * AKT + 8 * (((32 + l32) >> 3) ^ (qr & 7)) + (l32 & 7)] = f2h_bits(p1);
+		}
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // wave-local LDS transpose: in-order per wave
+		// ---- O += P V
+#pragma unroll
+		for (int s = 0; s < AKT / 16; ++s) {
+			const int kcnk = 2 * s + hh;
+			const half8_t pa = *(const half8_t *)(ps + l32 * AKT + 8 * (kcnk ^ (l32 & 7)));
+#pragma unroll
+			for (int jd = 0; jd < D / 32; ++jd) {
+				const int d = 32 * jd + l32;
+				const half8_t vb = *(const half8_t *)(Vt + d * AKT + 8 * (kcnk ^ (d & 7)));
+				o[jd] = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa, vb, o[jd], 0, 0, 0);
+			}
+		}
+		__syncthreads(); // Ks / Vt / Ps reused by the next tile
+	}
+	// ---- normalise and store O[query][h * D + d] (f16, the Wo GEMM's A operand)
+#pragma unroll
+	for (int r = 0; r < 16; ++r) {
+		const int qrow = qw0 + crow(r, lane);
+		if (qrow >= T)
+			continue;
+		const float inv = 1.0f / l_r[r];
+#pragma unroll
+		for (int jd = 0; jd < D / 32; ++jd)
+			O[(size_t)qrow * q_dim + h * D + 32 * jd + l32] = f2h_bits(o[jd][r] * inv);
+	}
+}
+
+// ---------------------------------------------------------------- row kernels
+// X[t] = f32(E[token[t]])  (copy_embedding, infer.cu:632-640)
+template <class WT>
+__global__ __launch_bounds__(256) void embed_rows_kernel(const int *__restrict__ tokens, const void *__restrict__ emb,
+                                                         int dim, float *__restrict__ X) {
+	const int t = blockIdx.x;
+	const char *row = (const char *)emb + (size_t)tokens[t] * dim * WT::BYTES;
+	for (int i = threadIdx.x * WT::EPL; i < dim; i += blockDim.x * WT::EPL) {
+		float f[WT::EPL];
+		WT::unpack(load16(row + (size_t)i * WT::BYTES), f);
+#pragma unroll
+		for (int e = 0; e < WT::EPL; ++e)
+			X[(size_t)t * dim + i + e] = f[e];
+	}
+}
+
+// Xn[t] = f16(rmsnorm(X[t]) * w)  (rmsnorm, infer.cpp:134-144 statement order)
+__global__ __launch_bounds__(256) void rmsnorm_rows_kernel(const float *__restrict__ X, const float *__restrict__ w,
+                                                           int dim, float eps, uint16_t *__restrict__ Xn) {
+	__shared__ float red[4];
+	const int t = blockIdx.x;
+	const float *x = X + (size_t)t * dim;
+	float ss = 0.0f;
+	for (int i = threadIdx.x * 4; i < dim; i += 256 * 4) {
+		const float4_t v = *(const float4_t *)(x + i);
+		ss += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+	}
+	ss = wave_sum(ss);
+	if ((threadIdx.x & 63) == 0)
+		red[threadIdx.x >> 6] = ss;
+	__syncthreads();
+	const float tot = red[0] + red[1] + red[2] + red[3];
+	const float scale = 1.0f / sqrtf(tot / dim + eps);
+	for (int i = threadIdx.x * 4; i < dim; i += 256 * 4) {
+		const float4_t v = *(const float4_t *)(x + i);
+		const float4_t g = *(const float4_t *)(w + i);
+		uint16_t *o = Xn + (size_t)t * dim + i;
+		o[0] = f2h_bits(v[0] * scale * g[0]);
+		o[1] = f2h_bits(v[1] * scale * g[1]);
+		o[2] = f2h_bits(v[2] * scale * g[2]);
+		o[3] = f2h_bits(v[3] * scale * g[3]);
+	}
+}
+
+// log p(target) per row from the vocab-tile partials: M = max, S = sum_i s_i e^(m_i - M)
+__global__ __launch_bounds__(256) void logprob_kernel(const float *__restrict__ pmax, const float *__restrict__ psum,
+                                                      const float *__restrict__ tgt_logit,
+                                                      const int *__restrict__ targets, int M, int ntiles,
+                                                      float *__restrict__ out) {
+	__shared__ float red[4];
+	const int m = blockIdx.x;
+	float mx = -FLT_MAX;
+	for (int i = threadIdx.x; i < ntiles; i += 256)
+		mx = fmaxf(mx, pmax[(size_t)m * ntiles + i]);
+	mx = wave_max(mx);
+	if ((threadIdx.x & 63) == 0)
+		red[threadIdx.x >> 6] = mx;
+	__syncthreads();
+	mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+	__syncthreads();
+	float s = 0.0f;
+	for (int i = threadIdx.x; i < ntiles; i += 256)
+		s += psum[(size_t)m * ntiles + i] * expf(pmax[(size_t)m * ntiles + i] - mx);
+	s = wave_sum(s);
+	if ((threadIdx.x & 63) == 0)
+		red[threadIdx.x >> 6] = s;
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		const float tot = red[0] + red[1] + red[2] + red[3];
+		out[m] = targets[m] >= 0 ? tgt_logit[m] - mx - logf(tot) : 0.0f;
+	}
+}
+
+} // namespace pf

@@ -1,0 +1,281 @@
+// prefill.hip — C ABI of the batched prefill / perplexity path (prefill.h):
+// yalm_prefill (prompt hydration + per-position log p(next), replacing the
+// reference's position-by-position loop in main.cpp:128-200 / 102-112) and
+// its kernel-level test hooks (yalm_gemm_f16, yalm_attn_prefill).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "decoder.h"
+#include "prefill.h"
+
+namespace {
+
+int pf_alloc(yalm_decoder_s *d, void **p, size_t bytes) {
+	HIPCHK(hipMalloc(p, bytes ? bytes : 4));
+	d->dev_allocs.push_back(*p);
+	return YALM_OK;
+}
+
+template <class EPI, int NB>
+int launch_gemm(const uint16_t *A, int M, int K, pf::BSrc b0, pf::BSrc b1, int N, const EPI &epi, hipStream_t st) {
+	auto kern = pf::gemm_nt_kernel<EPI, NB>;
+	const size_t lds = (size_t)2 * (1 + NB) * pf::TILE * sizeof(uint16_t);
+	static bool attr_set = false; // one per template instance
+	if (!attr_set) {
+		HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+		attr_set = true;
+	}
+	const int nwg = ((M + pf::BM - 1) / pf::BM) * (N / pf::BN);
+	hipLaunchKernelGGL(kern, dim3(nwg), dim3(pf::THREADS), lds, st, A, M, K, b0, b1, N, epi);
+	HIPCHK(hipGetLastError());
+	return YALM_OK;
+}
+
+pf::BSrc one(const void *w, int rows) {
+	pf::BSrc b{};
+	b.p[0] = b.p[1] = b.p[2] = (const uint16_t *)w;
+	b.end[0] = b.end[1] = b.end[2] = rows;
+	return b;
+}
+
+int launch_attn_prefill(const uint16_t *Q, const uint16_t *kc, const uint16_t *vc, int T, int pos0, int n_heads,
+                        int n_kv, int head_dim, uint16_t *O, hipStream_t st) {
+	const dim3 grid((T + pf::AQ - 1) / pf::AQ, n_heads);
+	if (head_dim == 128)
+		pf::attn_prefill_kernel<128><<<grid, pf::THREADS, 0, st>>>(Q, kc, vc, T, pos0, n_heads, n_kv, O);
+	else if (head_dim == 64)
+		pf::attn_prefill_kernel<64><<<grid, pf::THREADS, 0, st>>>(Q, kc, vc, T, pos0, n_heads, n_kv, O);
+	else {
+		set_err("prefill attention: head_dim must be 64 or 128");
+		return YALM_ERR_UNSUPPORTED;
+	}
+	HIPCHK(hipGetLastError());
+	return YALM_OK;
+}
+
+int check_prefill_shape(const yalm_config &c) {
+	const int q_dim = c.n_heads * c.head_dim, kv_dim = c.n_kv_heads * c.head_dim;
+	if (c.weight_dtype != YALM_F16) {
+		set_err("yalm_prefill: f16 weights only (MFMA f16 operands)");
+		return YALM_ERR_UNSUPPORTED;
+	}
+	if (c.dim % pf::BN || c.dim % pf::BK || c.hidden_dim % pf::BN || c.hidden_dim % pf::BK || q_dim % pf::BN ||
+	    q_dim % pf::BK || kv_dim % pf::BN || c.vocab_size % pf::BN || (c.head_dim != 64 && c.head_dim != 128)) {
+		set_err("yalm_prefill: dims must be multiples of 128 and head_dim 64 or 128");
+		return YALM_ERR_UNSUPPORTED;
+	}
+	return YALM_OK;
+}
+
+int ensure_bufs(yalm_decoder_s *d) {
+	PrefillBufs &b = d->pf;
+	if (b.cap)
+		return YALM_OK;
+	const yalm_config &c = d->c;
+	const size_t cap = (size_t)c.max_seq_len, q_dim = (size_t)c.n_heads * c.head_dim;
+	const size_t ntiles = (size_t)c.vocab_size / pf::BN;
+	TRY(pf_alloc(d, (void **)&b.X, cap * c.dim * 4));
+	TRY(pf_alloc(d, (void **)&b.Xn, cap * c.dim * 2));
+	TRY(pf_alloc(d, (void **)&b.Q, cap * q_dim * 2));
+	TRY(pf_alloc(d, (void **)&b.O, cap * q_dim * 2));
+	TRY(pf_alloc(d, (void **)&b.H, cap * c.hidden_dim * 2));
+	TRY(pf_alloc(d, (void **)&b.tok, cap * 4));
+	TRY(pf_alloc(d, (void **)&b.tgt, cap * 4));
+	TRY(pf_alloc(d, (void **)&b.pmax, cap * ntiles * 4));
+	TRY(pf_alloc(d, (void **)&b.psum, cap * ntiles * 4));
+	TRY(pf_alloc(d, (void **)&b.tgt_logit, cap * 4));
+	TRY(pf_alloc(d, (void **)&b.lp, cap * 4));
+	b.cap = (int)cap;
+	return YALM_OK;
+}
+
+template <int ACT>
+int enqueue_glu(yalm_decoder_s *d, const yalm_block_weights &w, int T) {
+	const yalm_config &c = d->c;
+	pf::EpiGlu<ACT> e;
+	e.h = d->pf.H;
+	e.ldh = c.hidden_dim;
+	e.M = T;
+	return launch_gemm<pf::EpiGlu<ACT>, 2>(d->pf.Xn, T, c.dim, one(w.w1, c.hidden_dim), one(w.w3, c.hidden_dim),
+	                                       c.hidden_dim, e, d->stream);
+}
+
+// The whole prefill on d->stream: T rows at positions pos0 .. pos0 + T - 1.
+int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
+	const yalm_config &c = d->c;
+	PrefillBufs &b = d->pf;
+	hipStream_t st = d->stream;
+	const int q_dim = c.n_heads * c.head_dim, kv_dim = c.n_kv_heads * c.head_dim;
+	pf::embed_rows_kernel<WF16><<<T, 256, 0, st>>>(b.tok, d->emb, c.dim, b.X);
+	HIPCHK(hipGetLastError());
+	for (int l = 0; l < c.n_layers; ++l) {
+		const yalm_block_weights &w = d->b[l];
+		pf::rmsnorm_rows_kernel<<<T, 256, 0, st>>>(b.X, w.rms_att, c.dim, c.norm_eps, b.Xn);
+		HIPCHK(hipGetLastError());
+		{
+			pf::BSrc qkv{};
+			qkv.p[0] = (const uint16_t *)w.wq;
+			qkv.p[1] = (const uint16_t *)w.wk;
+			qkv.p[2] = (const uint16_t *)w.wv;
+			qkv.end[0] = q_dim;
+			qkv.end[1] = q_dim + kv_dim;
+			qkv.end[2] = q_dim + 2 * kv_dim;
+			pf::EpiQKV e;
+			e.q = b.Q;
+			e.kc = w.key_cache;
+			e.vc = w.value_cache;
+			e.inv_freq = d->inv_freq;
+			e.M = T;
+			e.q_dim = q_dim;
+			e.kv_dim = kv_dim;
+			e.head_dim = c.head_dim;
+			e.pos0 = pos0;
+			e.clip = c.qkv_clip;
+			TRY((launch_gemm<pf::EpiQKV, 1>(b.Xn, T, c.dim, qkv, qkv, q_dim + 2 * kv_dim, e, st)));
+		}
+		TRY(launch_attn_prefill(b.Q, w.key_cache, w.value_cache, T, pos0, c.n_heads, c.n_kv_heads, c.head_dim, b.O,
+		                        st));
+		{
+			pf::EpiResidual e;
+			e.x = b.X;
+			e.ldx = c.dim;
+			e.M = T;
+			TRY((launch_gemm<pf::EpiResidual, 1>(b.O, T, q_dim, one(w.wo, c.dim), one(w.wo, c.dim), c.dim, e, st)));
+		}
+		pf::rmsnorm_rows_kernel<<<T, 256, 0, st>>>(b.X, w.rms_ffn, c.dim, c.norm_eps, b.Xn);
+		HIPCHK(hipGetLastError());
+		TRY(c.act == YALM_SILU ? enqueue_glu<1>(d, w, T) : enqueue_glu<0>(d, w, T));
+		{
+			pf::EpiResidual e;
+			e.x = b.X;
+			e.ldx = c.dim;
+			e.M = T;
+			TRY((launch_gemm<pf::EpiResidual, 1>(b.H, T, c.hidden_dim, one(w.w2, c.dim), one(w.w2, c.dim), c.dim, e,
+			                                     st)));
+		}
+	}
+	if (!want_lp)
+		return YALM_OK;
+	pf::rmsnorm_rows_kernel<<<T, 256, 0, st>>>(b.X, d->rms_final, c.dim, c.norm_eps, b.Xn);
+	HIPCHK(hipGetLastError());
+	const int ntiles = c.vocab_size / pf::BN;
+	pf::EpiLogits e;
+	e.pmax = b.pmax;
+	e.psum = b.psum;
+	e.tgt_logit = b.tgt_logit;
+	e.targets = b.tgt;
+	e.M = T;
+	e.ntiles = ntiles;
+	e.red = nullptr;
+	TRY((launch_gemm<pf::EpiLogits, 1>(b.Xn, T, c.dim, one(d->wcls, c.vocab_size), one(d->wcls, c.vocab_size),
+	                                   c.vocab_size, e, st)));
+	pf::logprob_kernel<<<T, 256, 0, st>>>(b.pmax, b.psum, b.tgt_logit, b.tgt, T, ntiles, b.lp);
+	HIPCHK(hipGetLastError());
+	return YALM_OK;
+}
+
+struct HostDev { // scoped device copy for the test hooks
+	void *p = nullptr;
+	~HostDev() {
+		if (p)
+			(void)hipFree(p);
+	}
+};
+int hd(HostDev &b, const void *host, size_t bytes) {
+	HIPCHK(hipMalloc(&b.p, bytes ? bytes : 4));
+	if (host)
+		HIPCHK(hipMemcpy(b.p, host, bytes, hipMemcpyHostToDevice));
+	else
+		HIPCHK(hipMemset(b.p, 0, bytes));
+	return YALM_OK;
+}
+
+} // namespace
+
+extern "C" int yalm_prefill(yalm_decoder d, const int *tokens, int n, int pos0, float *logprobs) {
+	ARGCHK(d && tokens && n > 0 && pos0 >= 0, "yalm_prefill: bad argument");
+	const yalm_config &c = d->c;
+	ARGCHK(pos0 + n <= c.max_seq_len, "yalm_prefill: pos0 + n must be <= max_seq_len (no sliding window in prefill)");
+	TRY(check_prefill_shape(c));
+	TRY(ensure_bufs(d));
+	PrefillBufs &b = d->pf;
+	std::vector<int> tgt(n);
+	for (int i = 0; i < n; ++i) {
+		ARGCHK(tokens[i] >= 0 && tokens[i] < c.vocab_size, "yalm_prefill: token id out of range");
+		tgt[i] = i + 1 < n ? tokens[i + 1] : -1;
+	}
+	HIPCHK(hipMemcpyAsync(b.tok, tokens, sizeof(int) * n, hipMemcpyHostToDevice, d->stream));
+	HIPCHK(hipMemcpyAsync(b.tgt, tgt.data(), sizeof(int) * n, hipMemcpyHostToDevice, d->stream));
+	TRY(enqueue_prefill(d, n, pos0, logprobs != nullptr));
+	if (logprobs)
+		HIPCHK(hipMemcpyAsync(logprobs, b.lp, sizeof(float) * n, hipMemcpyDeviceToHost, d->stream));
+	HIPCHK(hipStreamSynchronize(d->stream));
+	return YALM_OK;
+}
+
+extern "C" int yalm_prefill_time(yalm_decoder d, int n, int iters, float *avg_ms) {
+	ARGCHK(d && n > 0 && iters > 0 && avg_ms, "yalm_prefill_time: bad argument");
+	const yalm_config &c = d->c;
+	ARGCHK(n <= c.max_seq_len, "yalm_prefill_time: n > max_seq_len");
+	TRY(check_prefill_shape(c));
+	TRY(ensure_bufs(d));
+	std::vector<int> tok(n);
+	for (int i = 0; i < n; ++i)
+		tok[i] = (int)((1103515245u * (unsigned)i + 12345u) % (unsigned)c.vocab_size);
+	HIPCHK(hipMemcpy(d->pf.tok, tok.data(), sizeof(int) * n, hipMemcpyHostToDevice));
+	for (int i = 0; i < n; ++i)
+		tok[i] = i + 1 < n ? tok[i + 1] : -1;
+	HIPCHK(hipMemcpy(d->pf.tgt, tok.data(), sizeof(int) * n, hipMemcpyHostToDevice));
+	TRY(enqueue_prefill(d, n, 0, true)); // warm-up
+	hipEvent_t e0, e1;
+	HIPCHK(hipEventCreate(&e0));
+	HIPCHK(hipEventCreate(&e1));
+	HIPCHK(hipEventRecord(e0, d->stream));
+	for (int i = 0; i < iters; ++i)
+		TRY(enqueue_prefill(d, n, 0, true));
+	HIPCHK(hipEventRecord(e1, d->stream));
+	HIPCHK(hipEventSynchronize(e1));
+	float ms = 0;
+	HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+	(void)hipEventDestroy(e0);
+	(void)hipEventDestroy(e1);
+	*avg_ms = ms / iters;
+	return YALM_OK;
+}
+
+extern "C" int yalm_gemm_f16(float *c, const uint16_t *a, const uint16_t *w, int M, int N, int K) {
+	ARGCHK(c && a && w && M > 0 && N > 0 && K > 0, "yalm_gemm_f16: bad argument");
+	ARGCHK(N % pf::BN == 0 && K % pf::BK == 0, "yalm_gemm_f16: N % 128 and K % 64 must be 0");
+	HostDev da, dw, dc;
+	TRY(hd(da, a, (size_t)M * K * 2));
+	TRY(hd(dw, w, (size_t)N * K * 2));
+	TRY(hd(dc, nullptr, (size_t)M * N * 4));
+	pf::EpiStoreF32 e;
+	e.c = (float *)dc.p;
+	e.ldc = N;
+	e.M = M;
+	TRY((launch_gemm<pf::EpiStoreF32, 1>((const uint16_t *)da.p, M, K, one(dw.p, N), one(dw.p, N), N, e, nullptr)));
+	HIPCHK(hipDeviceSynchronize());
+	HIPCHK(hipMemcpy(c, dc.p, (size_t)M * N * 4, hipMemcpyDeviceToHost));
+	return YALM_OK;
+}
+
+extern "C" int yalm_attn_prefill(uint16_t *o, const uint16_t *q, const uint16_t *kc, const uint16_t *vc, int T,
+                                 int pos0, int n_heads, int n_kv_heads, int head_dim) {
+	ARGCHK(o && q && kc && vc && T > 0 && pos0 >= 0 && n_kv_heads > 0 && n_heads % n_kv_heads == 0,
+	       "yalm_attn_prefill: bad argument");
+	const size_t q_dim = (size_t)n_heads * head_dim, kv = (size_t)(pos0 + T) * n_kv_heads * head_dim;
+	HostDev dq, dk, dv, dout;
+	TRY(hd(dq, q, T * q_dim * 2));
+	TRY(hd(dk, kc, kv * 2));
+	TRY(hd(dv, vc, kv * 2));
+	TRY(hd(dout, nullptr, T * q_dim * 2));
+	TRY(launch_attn_prefill((const uint16_t *)dq.p, (const uint16_t *)dk.p, (const uint16_t *)dv.p, T, pos0, n_heads,
+	                        n_kv_heads, head_dim, (uint16_t *)dout.p, nullptr));
+	HIPCHK(hipDeviceSynchronize());
+	HIPCHK(hipMemcpy(o, dout.p, T * q_dim * 2, hipMemcpyDeviceToHost));
+	return YALM_OK;
+}

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "attention.h"
+#include "decoder.h"
 #include "device_common.h"
 #include "gemv.h"
 #include "misc_kernels.h"
@@ -22,34 +23,9 @@
 // ------------------------------------------------------------------ errors
 static thread_local std::string g_err;
 
-static void set_err(const std::string &s) {
+void set_err(const std::string &s) {
 	g_err = s;
 }
-
-#define HIPCHK(expr)                                                                                                   \
-	do {                                                                                                               \
-		hipError_t e_ = (expr);                                                                                        \
-		if (e_ != hipSuccess) {                                                                                        \
-			set_err(std::string(#expr) + " failed: " + hipGetErrorString(e_) + " (" + __FILE__ + ":" +                 \
-			        std::to_string(__LINE__) + ")");                                                                   \
-			return YALM_ERR_HIP;                                                                                       \
-		}                                                                                                              \
-	} while (0)
-
-#define ARGCHK(cond, msg)                                                                                              \
-	do {                                                                                                               \
-		if (!(cond)) {                                                                                                 \
-			set_err(msg);                                                                                              \
-			return YALM_ERR_ARG;                                                                                       \
-		}                                                                                                              \
-	} while (0)
-
-#define TRY(expr)                                                                                                      \
-	do {                                                                                                               \
-		int r_ = (expr);                                                                                               \
-		if (r_ != YALM_OK)                                                                                             \
-			return r_;                                                                                                 \
-	} while (0)
 
 extern "C" const char *yalm_last_error(void) {
 	return g_err.c_str();
@@ -136,13 +112,7 @@ extern "C" int yalm_synth(void *device, size_t n, int dtype, uint64_t seed, floa
 }
 
 // ------------------------------------------------------------------ launch helpers
-// GEMV launch geometry (see gemv_stream_kernel). 0 = automatic.
-struct GemvCfg {
-	int threads = 0, U = 0, gpw = 0;
-};
-enum { GK_QKV = 0, GK_WO = 1, GK_GLU = 2, GK_W2 = 3, GK_CLS = 4, GK_N = 5 };
-
-static int device_cu_count() {
+int device_cu_count() {
 	static int n = 0;
 	if (!n) {
 		int dev = 0;
@@ -382,34 +352,6 @@ static int launch_attn(int head_dim, int n_heads, int n_kv, const float *q, cons
 	HIPCHK(hipGetLastError());
 	return YALM_OK;
 }
-
-// ------------------------------------------------------------------ decoder
-enum { GRAPH_HYDRATE = 0, GRAPH_LOGITS = 1, GRAPH_GREEDY = 2, N_GRAPHS = 3 };
-
-struct yalm_decoder_s {
-	yalm_config c{};
-	std::vector<yalm_block_weights> b;
-	const void *emb = nullptr;
-	const float *rms_final = nullptr;
-	const void *wcls = nullptr;
-	hipStream_t stream = nullptr;
-	bool own_stream = false;
-	StepState *step = nullptr;
-	float *x = nullptr, *q = nullptr, *xb2 = nullptr, *hb = nullptr, *part = nullptr, *logits = nullptr,
-	      *inv_freq = nullptr;
-	int *tokens = nullptr;
-	int tokens_cap = 0;
-	float *logits_pinned = nullptr;
-	std::vector<void *> dev_allocs;
-	hipGraph_t graph[N_GRAPHS] = {};
-	hipGraphExec_t exec[N_GRAPHS] = {};
-	unsigned *attn_counters = nullptr; // per-kv-head arrival tickets (zeroed; the last arriver resets)
-	GemvCfg gemv[GK_N];
-	bool eager = false;     // YALM_EAGER=1: launch kernels directly (profilers that mis-handle graph replay)
-	bool graph_sync = false; // YALM_GRAPH_SYNC=1: synchronise after every replay
-	int ablate = 0;          // YALM_ABLATE bitmask: skip qkv|attn|wo|glu|w2 (1|2|4|8|16), timing only
-	std::string kname;
-};
 
 template <class WT>
 static int enqueue_layer_t(yalm_decoder_s *d, int l) {

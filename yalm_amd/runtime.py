@@ -107,6 +107,10 @@ _sig("yalm_set_gemv_config", c_int, [c_void_p, c_int, c_int, c_int, c_int])
 _sig("yalm_matmul", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int])
 _sig("yalm_mha", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int])
 _sig("yalm_ffn", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int])
+_sig("yalm_prefill", c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p])
+_sig("yalm_prefill_time", c_int, [c_void_p, c_int, c_int, ctypes.POINTER(c_float)])
+_sig("yalm_gemm_f16", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int])
+_sig("yalm_attn_prefill", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int])
 
 EXPORTED = [
     "yalm_last_error", "yalm_set_device", "yalm_upload", "yalm_alloc", "yalm_download", "yalm_register_host",
@@ -114,6 +118,7 @@ EXPORTED = [
     "yalm_synth", "yalm_decoder_create", "yalm_decoder_destroy", "yalm_forward", "yalm_generate_greedy",
     "yalm_enqueue_greedy", "yalm_device_step", "yalm_block", "yalm_get_x", "yalm_set_x", "yalm_get_logits",
     "yalm_time_kernel", "yalm_kernel_name", "yalm_set_gemv_config", "yalm_matmul", "yalm_mha", "yalm_ffn",
+    "yalm_prefill", "yalm_prefill_time", "yalm_gemm_f16", "yalm_attn_prefill",
 ]
 
 HYDRATE_KV_CACHE, OUTPUT_LOGITS = 0, 1
@@ -164,6 +169,26 @@ def ffn(x, w1, w2, w3, act: int, dtype: int) -> np.ndarray:
     out = np.zeros(dim, np.float32)
     check(lib.yalm_ffn(_ptr(out), _ptr(x), _ptr(w1), _ptr(w2), _ptr(w3), hidden_dim, dim, act, dtype))
     return out
+
+
+def gemm_f16(a: np.ndarray, w: np.ndarray) -> np.ndarray:
+    """MFMA GEMM of the prefill path: a (M, K) f16 @ w (N, K)^T f16 -> (M, N) f32."""
+    a = np.ascontiguousarray(a, dtype=np.float16)
+    w = np.ascontiguousarray(w, dtype=np.float16)
+    (M, K), N = a.shape, w.shape[0]
+    c = np.zeros((M, N), np.float32)
+    check(lib.yalm_gemm_f16(_ptr(c), _ptr(a), _ptr(w), M, N, K))
+    return c
+
+
+def attn_prefill(q, kc, vc, T, pos0, n_heads, n_kv_heads, head_dim) -> np.ndarray:
+    """Causal GQA prefill attention: q (T, n_heads*D) f16, kc/vc (pos0+T, n_kv*D) f16 -> (T, n_heads*D) f16."""
+    q = np.ascontiguousarray(q, dtype=np.float16)
+    kc = np.ascontiguousarray(kc, dtype=np.float16)
+    vc = np.ascontiguousarray(vc, dtype=np.float16)
+    o = np.zeros((T, n_heads * head_dim), np.float16)
+    check(lib.yalm_attn_prefill(_ptr(o), _ptr(q), _ptr(kc), _ptr(vc), T, pos0, n_heads, n_kv_heads, head_dim))
+    return o
 
 
 # ------------------------------------------------------------- model + decoder
@@ -265,6 +290,19 @@ class Decoder:
             return out
         check(lib.yalm_forward(self.h, token, pos, mode, None))
         return None
+
+    def prefill(self, tokens, pos0: int = 0, logprobs: bool = True):
+        """Batched MFMA prefill of positions pos0.. (fills the KV cache); returns
+        log p(tokens[i+1] | ..tokens[i]) per position (last entry 0) or None."""
+        tok = np.ascontiguousarray(tokens, dtype=np.int32)
+        out = np.zeros(len(tok), np.float32) if logprobs else None
+        check(lib.yalm_prefill(self.h, _ptr(tok), len(tok), pos0, _ptr(out) if logprobs else None))
+        return out
+
+    def prefill_time(self, n: int, iters: int = 3) -> float:
+        ms = c_float()
+        check(lib.yalm_prefill_time(self.h, n, iters, ctypes.byref(ms)))
+        return ms.value
 
     def generate_greedy(self, token: int, pos: int, n: int) -> list:
         out = np.zeros(max(n, 1), np.int32)
