@@ -59,6 +59,7 @@ struct PrefillBufs {
 	int *tgt = nullptr;        // [cap] next-token targets (-1: none)
 	float *pmax = nullptr, *psum = nullptr; // [cap][vocab / 128] logits partials
 	float *tgt_logit = nullptr, *lp = nullptr; // [cap]
+	float *rope = nullptr;                     // [cap][head_dim / 2][2]
 };
 
 // ------------------------------------------------------------------ decoder

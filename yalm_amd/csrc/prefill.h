@@ -142,7 +142,7 @@ struct EpiQKV {
 	float *red = nullptr;
 	uint16_t *q;
 	uint16_t *kc, *vc;
-	const float *inv_freq;
+	const float *rope; // [M][head_dim / 2][2] (cos, sin) of pos * inv_freq (rope_table_kernel)
 	int M, q_dim, kv_dim, head_dim, pos0;
 	float clip;
 	template <int NB>
@@ -155,7 +155,7 @@ struct EpiQKV {
 				const int n = n0 + 32 * j + (lane & 31);
 				const bool is_v = n >= q_dim + kv_dim;
 				const int nn = n < q_dim ? n : (n < q_dim + kv_dim ? n - q_dim : n - q_dim - kv_dim);
-				const float freq = inv_freq[(nn % head_dim) >> 1];
+				const int fj = (nn % head_dim) >> 1;
 #pragma unroll
 				for (int r = 0; r < 16; ++r) {
 					float v = acc[0][i][j][r];
@@ -167,9 +167,8 @@ struct EpiQKV {
 					const int pos = pos0 + m;
 					float o = v;
 					if (!is_v) {
-						const float val = (float)pos * freq;
-						const float fcr = cosf(val), fci = sinf(val);
-						o = odd ? p * fci + v * fcr : v * fcr - p * fci;
+						const float2_t cs = *(const float2_t *)(rope + ((size_t)m * (head_dim >> 1) + fj) * 2);
+						o = odd ? p * cs[1] + v * cs[0] : v * cs[0] - p * cs[1];
 					}
 					if (n < q_dim)
 						q[(size_t)m * q_dim + n] = f2h_bits(o);
@@ -347,16 +346,46 @@ __global__ __launch_bounds__(THREADS) void gemm_nt_kernel(const uint16_t *__rest
 //   its B fragments are row reads)
 constexpr int AQ = 128, AKT = 64; // queries per workgroup, keys per tile
 
+// Dynamic LDS of attn_prefill_kernel<D>: K[2][AKT][D], V[2][AKT][D], P[4 waves][32][AKT] (f16).
+template <int D>
+constexpr size_t attn_prefill_lds() {
+	return (size_t)(4 * AKT * D + 4 * 32 * AKT) * 2;
+}
+
+// Stage one 64-key tile of K or V (rows key0.., kv head g) by LDS-DMA. Row r of
+// the lane-linear image holds source chunk c ^ sw(r): sw = r % (D/8) for K
+// (row reads of 16 B, conflict-spread over 16 rows) and (r & 3) << 1 for V
+// (ds_read_b64_tr_b16 reads 4 rows x 32 B: the 4 rows land on distinct banks).
+template <int D, bool ISV>
+__device__ __forceinline__ void stage_kv(uint16_t *dst, const uint16_t *__restrict__ src, int key0, int kv_rows,
+                                         int kv_dim, int g, int wave, int lane) {
+	constexpr int DCH = D / 8;
+	constexpr int RPI = 1024 / (D * 2); // rows per 1-KB wave-instruction
+	constexpr int NI = AKT / RPI / 4;   // instructions per wave
+#pragma unroll
+	for (int i = 0; i < NI; ++i) {
+		const int rb = wave * NI + i;
+		const int r = rb * RPI + lane / DCH;
+		const int c = lane % DCH;
+		const int sw = ISV ? ((r & 3) << 1) : (r % DCH);
+		const uint16_t *p = src + (size_t)min(key0 + r, kv_rows - 1) * kv_dim + g * D + 8 * (c ^ sw);
+		__builtin_amdgcn_global_load_lds((const void *)p, (YALM_LDS void *)(dst + rb * RPI * D), 16, 0, 0);
+	}
+}
+
+typedef short short4_t __attribute__((ext_vector_type(4)));
+
 template <int D>
 __global__ __launch_bounds__(THREADS) void attn_prefill_kernel(const uint16_t *__restrict__ Q,
                                                                const uint16_t *__restrict__ kc,
                                                                const uint16_t *__restrict__ vc, int T, int pos0,
                                                                int n_heads, int n_kv, uint16_t *__restrict__ O) {
-	static_assert(D % 16 == 0 && D <= 256, "head_dim");
-	constexpr int DCH = D / 8;                   // 16-byte chunks per K row
-	__shared__ __attribute__((aligned(16))) uint16_t Ks[AKT * D]; // [key][D], chunk ^ (key % DCH)
-	__shared__ __attribute__((aligned(16))) uint16_t Vt[D * AKT]; // [d][key], chunk ^ (d & 7)
-	__shared__ __attribute__((aligned(16))) uint16_t Ps[4][32 * AKT]; // per wave [query][key]
+	static_assert(D == 64 || D == 128, "head_dim");
+	constexpr int DCH = D / 8;
+	extern __shared__ __attribute__((aligned(16))) uint16_t asmem[];
+	uint16_t *const Kb = asmem;                 // [2][AKT * D]
+	uint16_t *const Vb = asmem + 2 * AKT * D;   // [2][AKT * D]
+	uint16_t *const Pb = asmem + 4 * AKT * D;   // [4][32 * AKT]
 	const int lane = threadIdx.x & 63, l32 = lane & 31, hh = lane >> 5;
 	const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 	const int qb = gridDim.x - 1 - blockIdx.x; // heaviest (latest) query blocks first
@@ -383,46 +412,26 @@ __global__ __launch_bounds__(THREADS) void attn_prefill_kernel(const uint16_t *_
 		m_r[r] = -FLT_MAX;
 		l_r[r] = 0.0f;
 	}
-	const int qmax_blk = min(qb * AQ + AQ, T) - 1;  // last query row of the block
-	const int ntile = (pos0 + qmax_blk) / AKT + 1;  // key tiles up to its position
-	uint16_t *ps = Ps[wave];
+	const int qmax_blk = min(qb * AQ + AQ, T) - 1; // last query row of the block
+	const int ntile = (pos0 + qmax_blk) / AKT + 1; // key tiles up to its position
+	uint16_t *ps = Pb + wave * 32 * AKT;
+	// transposed-read lane geometry (ds_read_b64_tr_b16: 16-lane groups, 4 rows x 16 columns)
+	const int gi = lane & 15, gq = gi >> 2, gp = gi & 3;
+	const int dgrp = 16 * ((lane >> 4) & 1); // d offset of this lane group within a 32-wide block
 
+	stage_kv<D, false>(Kb, kc, 0, kv_rows, kv_dim, g, wave, lane);
+	stage_kv<D, true>(Vb, vc, 0, kv_rows, kv_dim, g, wave, lane);
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	__syncthreads();
+	int cur = 0;
 	for (int kt = 0; kt < ntile; ++kt) {
 		const int key0 = kt * AKT;
-		// ---- stage K (LDS-DMA, lane-linear rows, swizzle on the source) and V^T (registers)
-		{
-			constexpr int ROWS_PER_INSTR = 1024 / (D * 2);
-#pragma unroll
-			for (int i = 0; i < AKT / ROWS_PER_INSTR / 4; ++i) {
-				const int rb = wave * (AKT / ROWS_PER_INSTR / 4) + i;
-				const int r = rb * ROWS_PER_INSTR + lane / DCH;
-				const int c = lane % DCH;
-				const uint16_t *src = kc + (size_t)min(key0 + r, kv_rows - 1) * kv_dim + g * D + 8 * (c ^ (r % DCH));
-				__builtin_amdgcn_global_load_lds((const void *)src, (YALM_LDS void *)(Ks + rb * ROWS_PER_INSTR * D), 16,
-				                                 0, 0);
-			}
-			// V^T: thread -> (key, 32-dim slab); 4 x 16-byte loads, 32 transposed 2-byte LDS writes
-			constexpr int SLABS = D / 32;
-			for (int e = threadIdx.x; e < AKT * SLABS; e += THREADS) {
-				const int key = e / SLABS, d0 = (e % SLABS) * 32;
-				const uint16_t *src = vc + (size_t)min(key0 + key, kv_rows - 1) * kv_dim + g * D + d0;
-#pragma unroll
-				for (int c = 0; c < 4; ++c) {
-					const u32x4_t v = load16(src + 8 * c);
-#pragma unroll
-					for (int w = 0; w < 4; ++w) {
-						const uint32_t pair = v[w];
-#pragma unroll
-						for (int half = 0; half < 2; ++half) {
-							const int d = d0 + 8 * c + 2 * w + half;
-							Vt[d * AKT + 8 * ((key >> 3) ^ (d & 7)) + (key & 7)] = (uint16_t)(pair >> (16 * half));
-						}
-					}
-				}
-			}
+		if (kt + 1 < ntile) { // next tile's LDS-DMA overlaps this tile's math
+			stage_kv<D, false>(Kb + (cur ^ 1) * AKT * D, kc, key0 + AKT, kv_rows, kv_dim, g, wave, lane);
+			stage_kv<D, true>(Vb + (cur ^ 1) * AKT * D, vc, key0 + AKT, kv_rows, kv_dim, g, wave, lane);
 		}
-		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-		__syncthreads();
+		const uint16_t *Ks = Kb + cur * AKT * D;
+		const uint16_t *Vs = Vb + cur * AKT * D;
 
 		// ---- S = Q K^T for this wave's 32 queries x 64 keys
 		f32x16_t sacc[2];
@@ -460,24 +469,43 @@ __global__ __launch_bounds__(THREADS) void attn_prefill_kernel(const uint16_t *_
 #pragma unroll
 			for (int jd = 0; jd < D / 32; ++jd)
 				o[jd][r] *= alpha;
-			const int qr = crow(r, lane); // P^T -> Ps[query][key]
+			const int qr = crow(r, lane); // P^T -> ps[query][key]
 			ps[qr * AKT + 8 * ((l32 >> 3) ^ (qr & 7)) + (l32 & 7)] = f2h_bits(p0);
 			ps[qr * AKT + 8 * (((32 + l32) >> 3) ^ (qr & 7)) + (l32 & 7)] = f2h_bits(p1);
 		}
 		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // wave-local LDS transpose: in-order per wave
-		// ---- O += P V
+		// ---- O += P V   (V B-fragments by hardware-transposed reads of the row-major V tile)
 #pragma unroll
 		for (int s = 0; s < AKT / 16; ++s) {
 			const int kcnk = 2 * s + hh;
 			const half8_t pa = *(const half8_t *)(ps + l32 * AKT + 8 * (kcnk ^ (l32 & 7)));
+			const int k0 = 16 * s + 8 * hh;
 #pragma unroll
 			for (int jd = 0; jd < D / 32; ++jd) {
-				const int d = 32 * jd + l32;
-				const half8_t vb = *(const half8_t *)(Vt + d * AKT + 8 * (kcnk ^ (d & 7)));
+				const int d = 32 * jd + dgrp + 4 * gp; // this lane's 4-column address
+				short4_t lo, hi;
+				{
+					const int key = k0 + gq;
+					lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+					    (YALM_LDS short4_t *)(Vs + key * D + 8 * ((d >> 3) ^ ((key & 3) << 1)) + (d & 7)));
+				}
+				{
+					const int key = k0 + 4 + gq;
+					hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+					    (YALM_LDS short4_t *)(Vs + key * D + 8 * ((d >> 3) ^ ((key & 3) << 1)) + (d & 7)));
+				}
+				half8_t vb;
+#pragma unroll
+				for (int e = 0; e < 4; ++e) {
+					vb[e] = __builtin_bit_cast(_Float16, (short)lo[e]);
+					vb[4 + e] = __builtin_bit_cast(_Float16, (short)hi[e]);
+				}
 				o[jd] = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa, vb, o[jd], 0, 0, 0);
 			}
 		}
-		__syncthreads(); // Ks / Vt / Ps reused by the next tile
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		__syncthreads(); // next tile landed; this tile's K / V / P reads are done
+		cur ^= 1;
 	}
 	// ---- normalise and store O[query][h * D + d] (f16, the Wo GEMM's A operand)
 #pragma unroll
@@ -534,6 +562,20 @@ __global__ __launch_bounds__(256) void rmsnorm_rows_kernel(const float *__restri
 		o[2] = f2h_bits(v[2] * scale * g[2]);
 		o[3] = f2h_bits(v[3] * scale * g[3]);
 	}
+}
+
+// RoPE (cos, sin) per prompt row and frequency, the decode path's exact
+// formula (angle = (float)pos * inv_freq[j]; cosf / sinf, infer.cpp:291-301):
+// computed once per prefill instead of 2 x 64 transcendentals per QKV element.
+__global__ __launch_bounds__(256) void rope_table_kernel(const float *__restrict__ inv_freq, int half_dim, int T,
+                                                         int pos0, float *__restrict__ rope) {
+	const int i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= T * half_dim)
+		return;
+	const int m = i / half_dim, j = i % half_dim;
+	const float val = (float)(pos0 + m) * inv_freq[j];
+	rope[2 * i] = cosf(val);
+	rope[2 * i + 1] = sinf(val);
 }
 
 // log p(target) per row from the vocab-tile partials: M = max, S = sum_i s_i e^(m_i - M)

@@ -44,10 +44,20 @@ pf::BSrc one(const void *w, int rows) {
 int launch_attn_prefill(const uint16_t *Q, const uint16_t *kc, const uint16_t *vc, int T, int pos0, int n_heads,
                         int n_kv, int head_dim, uint16_t *O, hipStream_t st) {
 	const dim3 grid((T + pf::AQ - 1) / pf::AQ, n_heads);
+	static bool attr_set = false;
+	if (!attr_set) {
+		HIPCHK(hipFuncSetAttribute((const void *)pf::attn_prefill_kernel<128>,
+		                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)pf::attn_prefill_lds<128>()));
+		HIPCHK(hipFuncSetAttribute((const void *)pf::attn_prefill_kernel<64>,
+		                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)pf::attn_prefill_lds<64>()));
+		attr_set = true;
+	}
 	if (head_dim == 128)
-		pf::attn_prefill_kernel<128><<<grid, pf::THREADS, 0, st>>>(Q, kc, vc, T, pos0, n_heads, n_kv, O);
+		pf::attn_prefill_kernel<128><<<grid, pf::THREADS, pf::attn_prefill_lds<128>(), st>>>(Q, kc, vc, T, pos0,
+		                                                                                       n_heads, n_kv, O);
 	else if (head_dim == 64)
-		pf::attn_prefill_kernel<64><<<grid, pf::THREADS, 0, st>>>(Q, kc, vc, T, pos0, n_heads, n_kv, O);
+		pf::attn_prefill_kernel<64><<<grid, pf::THREADS, pf::attn_prefill_lds<64>(), st>>>(Q, kc, vc, T, pos0,
+		                                                                                     n_heads, n_kv, O);
 	else {
 		set_err("prefill attention: head_dim must be 64 or 128");
 		return YALM_ERR_UNSUPPORTED;
@@ -88,6 +98,7 @@ int ensure_bufs(yalm_decoder_s *d) {
 	TRY(pf_alloc(d, (void **)&b.psum, cap * ntiles * 4));
 	TRY(pf_alloc(d, (void **)&b.tgt_logit, cap * 4));
 	TRY(pf_alloc(d, (void **)&b.lp, cap * 4));
+	TRY(pf_alloc(d, (void **)&b.rope, cap * c.head_dim * 4));
 	b.cap = (int)cap;
 	return YALM_OK;
 }
@@ -111,6 +122,9 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 	const int q_dim = c.n_heads * c.head_dim, kv_dim = c.n_kv_heads * c.head_dim;
 	pf::embed_rows_kernel<WF16><<<T, 256, 0, st>>>(b.tok, d->emb, c.dim, b.X);
 	HIPCHK(hipGetLastError());
+	const int half = c.head_dim / 2;
+	pf::rope_table_kernel<<<(T * half + 255) / 256, 256, 0, st>>>(d->inv_freq, half, T, pos0, b.rope);
+	HIPCHK(hipGetLastError());
 	for (int l = 0; l < c.n_layers; ++l) {
 		const yalm_block_weights &w = d->b[l];
 		pf::rmsnorm_rows_kernel<<<T, 256, 0, st>>>(b.X, w.rms_att, c.dim, c.norm_eps, b.Xn);
@@ -127,7 +141,7 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 			e.q = b.Q;
 			e.kc = w.key_cache;
 			e.vc = w.value_cache;
-			e.inv_freq = d->inv_freq;
+			e.rope = b.rope;
 			e.M = T;
 			e.q_dim = q_dim;
 			e.kv_dim = kv_dim;
