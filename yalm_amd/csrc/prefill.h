@@ -346,10 +346,10 @@ __global__ __launch_bounds__(THREADS) void gemm_nt_kernel(const uint16_t *__rest
 //   its B fragments are row reads)
 constexpr int AQ = 128, AKT = 64; // queries per workgroup, keys per tile
 
-// Dynamic LDS of attn_prefill_kernel<D>: K[2][AKT][D], V[2][AKT][D], P[4 waves][32][AKT] (f16).
+// Dynamic LDS of attn_prefill_kernel<D>: K[2][AKT][D], V[2][AKT][D] (f16).
 template <int D>
 constexpr size_t attn_prefill_lds() {
-	return (size_t)(4 * AKT * D + 4 * 32 * AKT) * 2;
+	return (size_t)(4 * AKT * D) * 2;
 }
 
 // Stage one 64-key tile of K or V (rows key0.., kv head g) by LDS-DMA. Row r of
@@ -375,6 +375,15 @@ __device__ __forceinline__ void stage_kv(uint16_t *dst, const uint16_t *__restri
 
 typedef short short4_t __attribute__((ext_vector_type(4)));
 
+// "Swapped" formulation (cdna_hip_programming.md §3, accumulator as the next
+// operand; Appendix B fused attention): S^T = K Q^T puts the query on the
+// lane and 32 of the tile's 64 keys in registers, so the softmax row max / sum
+// are register folds plus one permlane32 swap (no per-key cross-lane
+// reductions, no LDS transpose of P), and O^T += V^T P^T takes P^T straight
+// from the S^T accumulators (k order permuted: element e of lane half h is key
+// 16 s + 8 (e >> 2) + 4 h + (e & 3) of the 32-key block) with V^T fragments
+// from hardware-transposed LDS reads. O^T keeps the query on the lane too, so
+// the online-softmax rescale is one per-lane factor.
 template <int D>
 __global__ __launch_bounds__(THREADS) void attn_prefill_kernel(const uint16_t *__restrict__ Q,
                                                                const uint16_t *__restrict__ kc,
@@ -383,41 +392,37 @@ __global__ __launch_bounds__(THREADS) void attn_prefill_kernel(const uint16_t *_
 	static_assert(D == 64 || D == 128, "head_dim");
 	constexpr int DCH = D / 8;
 	extern __shared__ __attribute__((aligned(16))) uint16_t asmem[];
-	uint16_t *const Kb = asmem;                 // [2][AKT * D]
-	uint16_t *const Vb = asmem + 2 * AKT * D;   // [2][AKT * D]
-	uint16_t *const Pb = asmem + 4 * AKT * D;   // [4][32 * AKT]
+	uint16_t *const Kb = asmem;               // [2][AKT * D]
+	uint16_t *const Vb = asmem + 2 * AKT * D; // [2][AKT * D]
 	const int lane = threadIdx.x & 63, l32 = lane & 31, hh = lane >> 5;
 	const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 	const int qb = gridDim.x - 1 - blockIdx.x; // heaviest (latest) query blocks first
 	const int h = blockIdx.y, g = h / (n_heads / n_kv);
 	const int q_dim = n_heads * D, kv_dim = n_kv * D;
 	const int qw0 = qb * AQ + wave * 32; // this wave's first query row
-	const float scale = 1.0f / sqrtf((float)D);
+	const int qrow = qw0 + l32;          // this lane's query
+	const int qpos = pos0 + qrow;
+	// scores in log2 units: exp2(s * log2(e) / sqrt(D) - m)
+	const float sl2 = 1.4426950408889634f / sqrtf((float)D);
 	const int kv_rows = pos0 + T; // valid cache rows (masked keys past a query are never used)
 
-	half8_t qf[D / 16];
+	half8_t qf[D / 16]; // B operand of S^T = K Q^T: Q[query = l32][d = 16 s + 8 h ..]
 	{
-		const uint16_t *qp = Q + (size_t)min(qw0 + l32, T - 1) * q_dim + h * D + 8 * hh;
+		const uint16_t *qp = Q + (size_t)min(qrow, T - 1) * q_dim + h * D + 8 * hh;
 #pragma unroll
 		for (int s = 0; s < D / 16; ++s)
 			qf[s] = *(const half8_t *)(qp + 16 * s);
 	}
-	f32x16_t o[D / 32];
+	f32x16_t o[D / 32]; // O^T tiles: rows = d (32 jd + crow), column = query
 #pragma unroll
 	for (int jd = 0; jd < D / 32; ++jd)
 		o[jd] = f32x16_t{};
-	float m_r[16], l_r[16];
-#pragma unroll
-	for (int r = 0; r < 16; ++r) {
-		m_r[r] = -FLT_MAX;
-		l_r[r] = 0.0f;
-	}
+	float m = -FLT_MAX, l = 0.0f;
 	const int qmax_blk = min(qb * AQ + AQ, T) - 1; // last query row of the block
 	const int ntile = (pos0 + qmax_blk) / AKT + 1; // key tiles up to its position
-	uint16_t *ps = Pb + wave * 32 * AKT;
 	// transposed-read lane geometry (ds_read_b64_tr_b16: 16-lane groups, 4 rows x 16 columns)
 	const int gi = lane & 15, gq = gi >> 2, gp = gi & 3;
-	const int dgrp = 16 * ((lane >> 4) & 1); // d offset of this lane group within a 32-wide block
+	const int dgrp = 16 * ((lane >> 4) & 1);
 
 	stage_kv<D, false>(Kb, kc, 0, kv_rows, kv_dim, g, wave, lane);
 	stage_kv<D, true>(Vb, vc, 0, kv_rows, kv_dim, g, wave, lane);
@@ -433,90 +438,90 @@ __global__ __launch_bounds__(THREADS) void attn_prefill_kernel(const uint16_t *_
 		const uint16_t *Ks = Kb + cur * AKT * D;
 		const uint16_t *Vs = Vb + cur * AKT * D;
 
-		// ---- S = Q K^T for this wave's 32 queries x 64 keys
-		f32x16_t sacc[2];
+		// ---- S^T = K Q^T: two 32-key blocks; register r of block j is key key0 + 32 j + crow(r, lane)
+		f32x16_t st[2];
 #pragma unroll
 		for (int j = 0; j < 2; ++j) {
-			sacc[j] = f32x16_t{};
+			st[j] = f32x16_t{};
 			const int kr = 32 * j + l32;
 #pragma unroll
 			for (int s = 0; s < D / 16; ++s) {
 				const int kcnk = 2 * s + hh;
-				const half8_t kb = *(const half8_t *)(Ks + kr * D + 8 * (kcnk ^ (kr % DCH)));
-				sacc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(qf[s], kb, sacc[j], 0, 0, 0);
+				const half8_t ka = *(const half8_t *)(Ks + kr * D + 8 * (kcnk ^ (kr % DCH)));
+				st[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ka, qf[s], st[j], 0, 0, 0);
 			}
 		}
-		// ---- online softmax; row (query) of register r: qw0 + crow(r, lane); key column: key0 + 32 j + l32
+		// ---- online softmax for this lane's query (causal mask on the diagonal tiles)
+		const bool diag = key0 + AKT - 1 > pos0 + qw0;
+		float mx = -FLT_MAX;
 #pragma unroll
-		for (int r = 0; r < 16; ++r) {
-			const int qpos = pos0 + qw0 + crow(r, lane);
-			float s0 = sacc[0][r] * scale, s1 = sacc[1][r] * scale;
-			if (key0 + l32 > qpos)
-				s0 = -FLT_MAX;
-			if (key0 + 32 + l32 > qpos)
-				s1 = -FLT_MAX;
-			float mx = fmaxf(s0, s1);
-			mx = row16_max(mx);
-			mx = fmaxf(mx, xor16(mx));
-			const float mn = fmaxf(m_r[r], mx);
-			const float alpha = expf(m_r[r] - mn);
-			const float p0 = expf(s0 - mn), p1 = expf(s1 - mn);
-			float ls = p0 + p1;
-			ls = row16_sum(ls);
-			ls += xor16(ls);
-			l_r[r] = l_r[r] * alpha + ls;
-			m_r[r] = mn;
+		for (int j = 0; j < 2; ++j)
 #pragma unroll
-			for (int jd = 0; jd < D / 32; ++jd)
-				o[jd][r] *= alpha;
-			const int qr = crow(r, lane); // P^T -> ps[query][key]
-			ps[qr * AKT + 8 * ((l32 >> 3) ^ (qr & 7)) + (l32 & 7)] = f2h_bits(p0);
-			ps[qr * AKT + 8 * (((32 + l32) >> 3) ^ (qr & 7)) + (l32 & 7)] = f2h_bits(p1);
-		}
-		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // wave-local LDS transpose: in-order per wave
-		// ---- O += P V   (V B-fragments by hardware-transposed reads of the row-major V tile)
-#pragma unroll
-		for (int s = 0; s < AKT / 16; ++s) {
-			const int kcnk = 2 * s + hh;
-			const half8_t pa = *(const half8_t *)(ps + l32 * AKT + 8 * (kcnk ^ (l32 & 7)));
-			const int k0 = 16 * s + 8 * hh;
-#pragma unroll
-			for (int jd = 0; jd < D / 32; ++jd) {
-				const int d = 32 * jd + dgrp + 4 * gp; // this lane's 4-column address
-				short4_t lo, hi;
-				{
-					const int key = k0 + gq;
-					lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-					    (YALM_LDS short4_t *)(Vs + key * D + 8 * ((d >> 3) ^ ((key & 3) << 1)) + (d & 7)));
-				}
-				{
-					const int key = k0 + 4 + gq;
-					hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-					    (YALM_LDS short4_t *)(Vs + key * D + 8 * ((d >> 3) ^ ((key & 3) << 1)) + (d & 7)));
-				}
-				half8_t vb;
-#pragma unroll
-				for (int e = 0; e < 4; ++e) {
-					vb[e] = __builtin_bit_cast(_Float16, (short)lo[e]);
-					vb[4 + e] = __builtin_bit_cast(_Float16, (short)hi[e]);
-				}
-				o[jd] = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa, vb, o[jd], 0, 0, 0);
+			for (int r = 0; r < 16; ++r) {
+				float v = st[j][r] * sl2;
+				if (diag && key0 + 32 * j + crow(r, lane) > qpos)
+					v = -FLT_MAX;
+				st[j][r] = v;
+				mx = fmaxf(mx, v);
 			}
-		}
-		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-		__syncthreads(); // next tile landed; this tile's K / V / P reads are done
-		cur ^= 1;
-	}
-	// ---- normalise and store O[query][h * D + d] (f16, the Wo GEMM's A operand)
+		mx = fmaxf(mx, xor32(mx)); // the other lane half holds the other 32 keys
+		const float mn = fmaxf(m, mx);
+		const float alpha = __builtin_amdgcn_exp2f(m - mn);
+		m = mn;
+		float ls = 0.0f;
+		half8_t pb[2][2]; // P^T fragments: [block j][k-step s]
 #pragma unroll
-	for (int r = 0; r < 16; ++r) {
-		const int qrow = qw0 + crow(r, lane);
-		if (qrow >= T)
-			continue;
-		const float inv = 1.0f / l_r[r];
+		for (int j = 0; j < 2; ++j)
+#pragma unroll
+			for (int r = 0; r < 16; ++r) {
+				const float p = __builtin_amdgcn_exp2f(st[j][r] - mn);
+				ls += p;
+				pb[j][r >> 3][r & 7] = (_Float16)p;
+			}
+		ls += xor32(ls);
+		l = l * alpha + ls;
 #pragma unroll
 		for (int jd = 0; jd < D / 32; ++jd)
-			O[(size_t)qrow * q_dim + h * D + 32 * jd + l32] = f2h_bits(o[jd][r] * inv);
+			o[jd] *= alpha;
+		// ---- O^T += V^T P^T
+#pragma unroll
+		for (int j = 0; j < 2; ++j)
+#pragma unroll
+			for (int s = 0; s < 2; ++s) {
+				const int klo = 32 * j + 16 * s + 4 * hh + gq; // keys of elements 0..3 (row gq of the 4-row block)
+#pragma unroll
+				for (int jd = 0; jd < D / 32; ++jd) {
+					const int d = 32 * jd + dgrp + 4 * gp;
+					const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+					    (YALM_LDS short4_t *)(Vs + klo * D + 8 * ((d >> 3) ^ ((klo & 3) << 1)) + (d & 7)));
+					const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((YALM_LDS short4_t *)(
+					    Vs + (klo + 8) * D + 8 * ((d >> 3) ^ (((klo + 8) & 3) << 1)) + (d & 7)));
+					half8_t va;
+#pragma unroll
+					for (int e = 0; e < 4; ++e) {
+						va[e] = __builtin_bit_cast(_Float16, (short)lo[e]);
+						va[4 + e] = __builtin_bit_cast(_Float16, (short)hi[e]);
+					}
+					o[jd] = __builtin_amdgcn_mfma_f32_32x32x16_f16(va, pb[j][s], o[jd], 0, 0, 0);
+				}
+			}
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		__syncthreads(); // next tile landed; this tile's K / V reads are done
+		cur ^= 1;
+	}
+	// ---- normalise and store O[query][h * D + d] (f16, the Wo GEMM's A operand); d = 32 jd + crow(r)
+	if (qrow < T) {
+		const float inv = 1.0f / l;
+		uint16_t *op = O + (size_t)qrow * q_dim + h * D;
+#pragma unroll
+		for (int jd = 0; jd < D / 32; ++jd)
+#pragma unroll
+			for (int r4 = 0; r4 < 4; ++r4) { // registers 4 r4 .. 4 r4 + 3 are 4 consecutive d
+				const int d = 32 * jd + 8 * r4 + 4 * hh;
+				uint32_t w0 = (uint32_t)f2h_bits(o[jd][4 * r4 + 0] * inv) | ((uint32_t)f2h_bits(o[jd][4 * r4 + 1] * inv) << 16);
+				uint32_t w1 = (uint32_t)f2h_bits(o[jd][4 * r4 + 2] * inv) | ((uint32_t)f2h_bits(o[jd][4 * r4 + 3] * inv) << 16);
+				*(uint2 *)(op + d) = make_uint2(w0, w1);
+			}
 	}
 }
 
