@@ -3,6 +3,8 @@ the reference-converted fixture (CPU), and the yalm CLI end to end on the
 GPU against the oracle's greedy tokens (the `-d cpu ... -t 0` contract of
 BASELINE config 1/2 on a tiny model)."""
 import os
+import re
+import sys
 import subprocess
 
 import numpy as np
@@ -99,3 +101,63 @@ def test_cli_greedy_matches_oracle(host_built, golden_dir, fname, context):
         lg = om.forward(nt, pos, 1)
         pos += 1
     assert got == ref
+
+
+def _prefill_yalm(tmp_path):
+    """A tiny model whose shapes have the batched-prefill path (dims multiple
+    of 128, head_dim 64), converted by our own converter."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import make_golden as G
+    from yalm_amd import convert
+
+    hf = dict(G.TINY_HF, hidden_size=256, intermediate_size=512, num_attention_heads=4, num_key_value_heads=2,
+              max_position_embeddings=256)
+    d = tmp_path / "hf"
+    G.write_hf_dir(str(d), hf=hf, seed=11)
+    out = tmp_path / "pf.yalm"
+    convert.convert(str(d), str(out), "fp16")
+    return str(out)
+
+
+PPL_TEXT = ("the sky is blue and the grass is green and the sun is yellow here we go there and back again "
+            "remember this important info the pass key is hidden inside a lot of irrelevant text")
+
+
+@pytest.mark.gpu
+def test_cli_perplexity_prefill_matches_sequential(host_built, tmp_path):
+    """-m perplexity through the batched MFMA prefill vs the reference's
+    position-by-position loop (YALM_NO_PREFILL=1) on the same file and text:
+    mean log p per position within 0.01 nats (f16 MFMA activations vs f32;
+    the random-weight model is very peaked, so ppl itself is ~1e11)."""
+    path = _prefill_yalm(tmp_path)
+    exe = os.path.join(host_built, "yalm")
+
+    def ppl(extra_env):
+        r = subprocess.run([exe, path, "-d", "hip", "-m", "perplexity", "-i", PPL_TEXT], capture_output=True,
+                           env=dict(os.environ, **extra_env), timeout=120)
+        assert r.returncode == 0, r.stderr.decode()
+        out = r.stdout.decode()
+        m = re.search(r"perplexity: ([0-9.eE+-]+)", out)
+        assert m, out
+        return float(m.group(1)), out
+
+    p_batched, out_b = ppl({})
+    p_seq, _ = ppl({"YALM_NO_PREFILL": "1"})
+    assert "batched prefill" in out_b
+    assert abs(np.log(p_batched) - np.log(p_seq)) < 0.01, (p_batched, p_seq)
+
+
+@pytest.mark.gpu
+def test_cli_completion_prefill_same_tokens(host_built, tmp_path):
+    """Prompt hydration by batched prefill then greedy decode == the all-decode run."""
+    path = _prefill_yalm(tmp_path)
+    exe = os.path.join(host_built, "yalm")
+
+    def toks(extra_env):
+        r = subprocess.run([exe, path, "-d", "hip", "-m", "c", "-t", "0", "-n", "24", "-i", PPL_TEXT[:80]],
+                           capture_output=True, env=dict(os.environ, YALM_PRINT_TOKENS="1", **extra_env), timeout=120)
+        assert r.returncode == 0, r.stderr.decode()
+        line = [l for l in r.stderr.decode().split("\n") if l.startswith("TOKENS:")][0]
+        return line
+
+    assert toks({}) == toks({"YALM_NO_PREFILL": "1"})

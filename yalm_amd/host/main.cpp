@@ -2,6 +2,7 @@
 // /root/reference/src/main.cpp:17-428): completion, perplexity and passkey,
 // -d device switch (cpu | cuda | hip prefixes), -m -n -t -i -f -T -l.
 // -t 0 runs the greedy loop with the argmax on the device.
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -93,7 +94,17 @@ static void run_completion(const std::string &path, const std::string &device, c
 	const uint64_t start = now_ms();
 	size_t read_bytes = 0;
 	int next = 0;
-	for (size_t pos = 0; pos < encoding.size(); ++pos) {
+	// hydrate all but the last prompt token in one batched prefill when the
+	// model has that path (yalm_prefill); the last token goes through the
+	// per-token forward, which produces its logits / greedy argmax
+	size_t first = 0;
+	if (encoding.size() >= 2 && (int)encoding.size() - 1 <= model.config->max_seq_len &&
+	    model.prefill(state, encoding.data(), (int)encoding.size() - 1, 0, nullptr)) {
+		first = encoding.size() - 1;
+		for (size_t pos = 0; pos < first; ++pos)
+			read_bytes += model.config->active_bytes(pos);
+	}
+	for (size_t pos = first; pos < encoding.size(); ++pos) {
 		const bool last = pos + 1 == encoding.size();
 		if (last && greedy)
 			next = model.forward_greedy(state, encoding[pos], (int)pos);
@@ -148,7 +159,22 @@ static void run_perplexity(const std::string &path, const std::string &device, c
 	const uint64_t start = now_ms();
 	size_t read_bytes = 0;
 	const size_t N = encoding.size() - 1;
-	for (size_t pos = 0; pos + 1 < encoding.size(); ++pos) {
+	// positions inside the context window in one batched prefill (per-position
+	// log p from a vocab-tiled log-softmax on the device); the rest, past
+	// max_seq_len (sliding window), position by position as in the reference
+	size_t pos = 0;
+	const size_t B = std::min(encoding.size(), (size_t)model.config->max_seq_len);
+	std::vector<float> lps(B);
+	if (B >= 2 && model.prefill(state, encoding.data(), (int)B, 0, lps.data())) {
+		for (; pos + 1 < B; ++pos) {
+			const double lp = lps[pos];
+			sum_logprob += lp;
+			ss_logprob += lp * lp;
+			read_bytes += model.config->active_bytes(pos);
+		}
+		std::cout << "\r Computing perplexity..." << pos << "/" << N << " (batched prefill)" << std::flush;
+	}
+	for (; pos + 1 < encoding.size(); ++pos) {
 		std::cout << "\r Computing perplexity..." << pos + 1 << "/" << N << std::flush;
 		model.forward(state, encoding[pos], (int)pos);
 		read_bytes += model.config->active_bytes(pos);

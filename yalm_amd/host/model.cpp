@@ -1,5 +1,7 @@
 #include "model.h"
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <cfloat>
 #include <cstdio>
@@ -258,6 +260,18 @@ void Model::forward(InferenceState &s, int token, int pos, InferenceMode mode) {
 	                   mode == InferenceMode::OUTPUT_LOGITS ? YALM_OUTPUT_LOGITS : YALM_HYDRATE_KV_CACHE,
 	                   mode == InferenceMode::OUTPUT_LOGITS ? s._logits : nullptr),
 	      "forward");
+}
+
+bool Model::prefill(InferenceState &s, const int *tokens, int n, int pos0, float *logprobs) {
+	const char *off = getenv("YALM_NO_PREFILL");
+	if ((off && atoi(off) != 0) || n <= 0)
+		return false;
+	ensure_decoder(s);
+	const int r = yalm_prefill(s._decoder, tokens, n, pos0, logprobs);
+	if (r == YALM_ERR_UNSUPPORTED)
+		return false;
+	check(r, "prefill");
+	return true;
 }
 
 int Model::forward_greedy(InferenceState &s, int token, int pos) {

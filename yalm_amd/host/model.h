@@ -122,6 +122,12 @@ struct Model {
 	// Greedy (-t 0) step on the device: forward + first-max argmax without
 	// copying logits to the host. Returns the next token.
 	int forward_greedy(InferenceState &s, int token, int pos);
+	// Batched MFMA prefill of tokens[0..n) at positions pos0.. (yalm_prefill):
+	// fills the KV cache; logprobs (may be null) gets log p(tokens[i+1]) per
+	// position. Returns false when this model's shape/dtype has no prefill
+	// path (f16 weights, dims multiple of 128, head_dim 64|128) or
+	// YALM_NO_PREFILL=1; the caller then runs the per-position forward.
+	bool prefill(InferenceState &s, const int *tokens, int n, int pos0, float *logprobs);
 	void cuda(); // Model::cuda (model.cpp:380-394)
 	void hip() {
 		cuda();
