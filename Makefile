@@ -11,7 +11,7 @@ HIP_HDRS = $(wildcard $(CSRC)/*.h) include/yalm_hip.h
 all: yalm_amd/libyalm_hip.so oracle host
 
 yalm_amd/libyalm_hip.so: $(HIP_OBJS)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(HIP_OBJS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(HIP_OBJS) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 build/%.o: $(CSRC)/%.hip $(HIP_HDRS)
 	@mkdir -p build

@@ -36,6 +36,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample budget")
     ap.add_argument("--kernel-iters", type=int, default=64)
+    ap.add_argument("--tp", action="store_true",
+                    help="tensor parallel over the launched ranks (one sequence, RCCL all-reduce) instead of replicas")
     return ap.parse_args()
 
 
@@ -105,23 +107,38 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    dev = local_rank
     if world > 1:
         import torch
         import torch.distributed as dist_mod
 
-        torch.cuda.set_device(local_rank)
-        dist_mod.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        # one rank per GPU; more ranks than GPUs (a 1-GPU rehearsal of the N > 1
+        # path) share devices round-robin
+        dev = local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+        if torch.cuda.device_count() >= world:
+            dist_mod.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist_mod.init_process_group("gloo")
         dist = dist_mod
 
     from yalm_amd import models as M
     from yalm_amd import runtime
 
-    runtime.check(runtime.lib.yalm_set_device(local_rank))
+    runtime.check(runtime.lib.yalm_set_device(dev))
     base = M.PRESETS[args.model]
     cfg = base.with_(weight_dtype=M.F16 if args.dtype == "fp16" else M.F8E5M2)
 
-    dm = runtime.DeviceModel.synthetic(cfg, seed=1)
-    dec = runtime.Decoder(dm)
+    if args.tp:
+        # one sequence sharded over all ranks (Megatron split, RCCL all-reduce in the graph)
+        dm = runtime.DeviceModel.synthetic(cfg, seed=1, tp=(rank, world))
+        uid = [runtime.tp_unique_id() if rank == 0 else None]
+        if dist is not None:
+            dist.broadcast_object_list(uid, src=0)
+        dec = runtime.Decoder(dm, tp_id=uid[0])
+    else:
+        dm = runtime.DeviceModel.synthetic(cfg, seed=1)
+        dec = runtime.Decoder(dm)
     prompt = [(7 * i + 1) % cfg.vocab_size for i in range(PROMPT_LEN)]
     for pos, t in enumerate(prompt[:-1]):
         dec.forward(t, pos, runtime.HYDRATE_KV_CACHE)
@@ -152,7 +169,8 @@ def main():
     if dist is not None:
         import torch
 
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([elapsed], dtype=torch.float64,
+                          device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     _, pos1 = dec.device_step()
@@ -162,16 +180,20 @@ def main():
     KID = 3
     avg_ms = dec.time_kernel(KID, args.kernel_iters)
     wb = M.DTYPE_BYTES[cfg.weight_dtype]
-    glu_bytes = 2 * cfg.hidden_dim * cfg.dim * wb + 2 * cfg.dim * 4 + cfg.hidden_dim * 4
+    hid_local = cfg.hidden_dim // (world if args.tp else 1)
+    glu_bytes = 2 * hid_local * cfg.dim * wb + 2 * cfg.dim * 4 + hid_local * 4
     achieved = glu_bytes / (avg_ms * 1e-3) / 1e9
     kname = dec.kernel_name(KID)
     traffic, traffic_src = pmc_traffic(kname, args.dtype)
 
-    toks = args.steps * world
+    toks = args.steps * (1 if args.tp else world)
     value = toks / elapsed
     kv_avg = (pos0 + pos1) / 2 + 1
     bytes_per_tok = cfg.weight_bytes_per_token() + cfg.kv_bytes_per_token(int(kv_avg))
-    step_gbs = bytes_per_tok * (args.steps / elapsed) / 1e9
+    step_gbs = bytes_per_tok * (args.steps / elapsed) / 1e9  # per sequence
+    n_seq = 1 if args.tp else world
+    agg_gbs = step_gbs * n_seq  # all GPUs
+    peak_all = HBM_PEAK_GBS * world
 
     out = {
         "metric": "decode tok/s Mistral-7B fp16 @1 GPU; % of HBM bytes/token roofline"
@@ -183,25 +205,26 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.tp else "weak",
         "vs_baseline": None,
         "dtype": "f16" if args.dtype == "fp16" else "f8e5m2",
         "data": "synthetic (random weights of the real Mistral-7B-v0.2 shape generated in HBM; "
                 f"{PROMPT_LEN}-token synthetic prompt; greedy argmax on device)",
         "config": {
-            "workload": f"{args.model} {args.dtype} batch-1 greedy decode, {args.steps} tokens/GPU, "
+            "workload": f"{args.model} {args.dtype} batch-1 greedy decode, {args.steps} tokens"
+                        f"{' (one sequence, tensor parallel)' if args.tp else '/GPU'}, "
                         f"kv_len {pos0 + 1}..{pos1}",
             "model": args.model,
             "global_batch": world,
             "seq_len": int(pos1),
-            "parallelism": f"replicas{world}" if world > 1 else "single",
+            "parallelism": (f"tp{world}" if args.tp else f"replicas{world}") if world > 1 else ("tp1" if args.tp else "single"),
         },
         "step_roofline": {
             "bytes_per_token": int(bytes_per_tok),
-            "achieved": round(step_gbs, 1),
-            "peak": HBM_PEAK_GBS,
+            "achieved": round(agg_gbs, 1),
+            "peak": peak_all,
             "unit": "GB/s",
-            "frac": round(step_gbs / HBM_PEAK_GBS, 4),
+            "frac": round(agg_gbs / peak_all, 4),
         },
         "roofline": {
             "bound": "hbm",

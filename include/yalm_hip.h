@@ -147,6 +147,29 @@ int yalm_set_gemv_config(yalm_decoder d, int kind, int threads, int unroll, int 
 /* Name of kernel_id's device function (to match rocprofv3 summaries). */
 const char *yalm_kernel_name(yalm_decoder d, int kernel_id);
 
+/* ---------------- tensor parallelism (BASELINE config 5) ----------------
+ * Megatron row/column split of one model over tp_size GPUs, one process per
+ * GPU: rank r holds Wq/Wk/Wv rows of heads [r*H/N, (r+1)*H/N) (kv heads
+ * likewise), Wo columns of those heads, W1/W3 rows and W2 columns
+ * [r*hidden/N, (r+1)*hidden/N), Wcls rows [r*vocab/N, ..); norms and the
+ * embedding are replicated. Each layer then needs two all-reduces of x
+ * (after Wo and after W2), captured in the per-token graph as RCCL
+ * ncclAllReduce over xGMI; the greedy argmax gathers one (value, index) pair
+ * per rank. Replaces the single-device forward of model.cpp:396-407 /
+ * infer.cu:1021-1128 for multi-GPU; the reference has no multi-GPU path. */
+/* 128-byte RCCL unique id, created by rank 0 and shared with the other ranks
+ * out of band (bench.py: torch.distributed broadcast). */
+int yalm_tp_unique_id(void *id_out);
+/* config: the FULL model; weights: this rank's shards as above (blocks as in
+ * yalm_decoder_create, KV caches for the local kv heads or null). Collective:
+ * every rank calls it concurrently (ncclCommInitRank). All yalm_forward /
+ * yalm_generate_greedy calls must then be made by every rank in lockstep;
+ * logits (full vocabulary) and greedy tokens are identical on all ranks. */
+int yalm_decoder_create_tp(const yalm_config *config, const yalm_model_weights *weights, int tp_rank, int tp_size,
+                           const void *unique_id, yalm_stream s, yalm_decoder *out);
+/* Device-to-device 2D copy (hipMemcpy2D): shard slicing of weights resident in HBM. */
+int yalm_copy_2d(void *dst, size_t dst_pitch, const void *src, size_t src_pitch, size_t width, size_t height);
+
 /* ---------------- batched prefill (MFMA): the perplexity / prompt path ----------------
  * Replaces the reference's position-by-position forward loop over a prompt
  * (main.cpp:128-200 `-m perplexity`, main.cpp:95-101 prompt hydration,

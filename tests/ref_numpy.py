@@ -40,7 +40,14 @@ def gelu(x):
 
 
 class RefModel:
-    def __init__(self, cfg: M.ModelConfig, tensors: dict):
+    """allreduce / allgather: tensor-parallel hooks (identity for one device):
+    with cfg = one rank's local dims and tensors = its shards (models.shard_array),
+    x += allreduce(Wo_r o_r) and logits = allgather(Wcls_r x) restate the
+    Megatron split of include/yalm_hip.h's yalm_decoder_create_tp."""
+
+    def __init__(self, cfg: M.ModelConfig, tensors: dict, allreduce=None, allgather=None):
+        self.allreduce = allreduce or (lambda v: v)
+        self.allgather = allgather or (lambda v: v)
         self.c = cfg
         self.t = {k: w64(v, cfg.weight_dtype) if v.ndim == 2 else v.astype(np.float64) for k, v in tensors.items()}
         # the KV cache is fp16 in the reference (model.h:299-300)
@@ -72,11 +79,11 @@ class RefModel:
             p = np.exp(s - s.max())
             p /= p.sum()
             out[h * c.head_dim:(h + 1) * c.head_dim] = p @ V[:, g, :]
-        x = x + t[n["wo"]] @ out
+        x = x + self.allreduce(t[n["wo"]] @ out)
         xb = rmsnorm(x, t[n["rms_ffn"]], c.norm_eps)
         a = t[n["w1"]] @ xb
         hb = (silu(a) if c.act == M.SILU else gelu(a)) * (t[n["w3"]] @ xb)
-        return x + t[n["w2"]] @ hb
+        return x + self.allreduce(t[n["w2"]] @ hb)
 
     def forward(self, token, pos):
         c = self.c
@@ -85,5 +92,5 @@ class RefModel:
         for l in range(c.n_layers):
             x = self.block(l, x, pos, kv_sink, kv_pos, kv_len)
         x = rmsnorm(x, self.t["model.norm.weight"], c.norm_eps)
-        wcls = self.t.get("model.output.weight", self.t["model.embed.weight"])
-        return wcls @ x
+        wcls = self.t.get("model.output.weight", self.t.get("tp.wcls", self.t["model.embed.weight"]))
+        return self.allgather(wcls @ x)

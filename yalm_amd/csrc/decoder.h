@@ -89,5 +89,14 @@ struct yalm_decoder_s {
 	int ablate = 0;          // YALM_ABLATE bitmask: skip qkv|attn|wo|glu|w2 (1|2|4|8|16), timing only
 	std::string kname;
 	PrefillBufs pf;
+	// tensor parallelism (yalm_decoder_create_tp): c holds the LOCAL shard dims
+	// (n_heads, n_kv_heads, hidden_dim, vocab_size divided by tp_size)
+	int tp_rank = 0, tp_size = 1;
+	void *comm = nullptr;            // ncclComm_t (RCCL); null = single-GPU decoder
+	int vocab_full = 0;              // unsharded vocabulary (logits all-gather, host copies)
+	float *xs = nullptr;             // [dim] Wo / W2 partial (+ x on rank 0), all-reduced into x
+	float *logits_local = nullptr;   // [vocab / tp] this rank's logits rows (== logits without TP)
+	float *amax = nullptr;           // [2] local argmax (value, global index as float bits)
+	float *amax_all = nullptr;       // [2 * tp_size]
 };
 

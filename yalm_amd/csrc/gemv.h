@@ -67,6 +67,31 @@ struct PResidual {
 	}
 };
 
+// out[row] = base[row] + acc: the tensor-parallel Wo / W2 partial of rank 0,
+// which also carries the residual into the all-reduce (other ranks: PStore).
+template <class WT, int R_>
+struct PAddTo {
+	static constexpr int R = R_;
+	const char *W;
+	int n;
+	float *out;
+	const float *base;
+	int n_groups;
+	__device__ __forceinline__ void prologue() const {}
+	__device__ __forceinline__ const char *row(int g, int r) const {
+		return W + (size_t)(g * R + r) * n * WT::BYTES;
+	}
+	__device__ __forceinline__ void finish(int g, const float *acc, int lane) const {
+		if (lane < R)
+			out[g * R + lane] = base[g * R + lane] + acc[lane];
+	}
+	__device__ __forceinline__ void finish_all(int g, const float *acc) const {
+#pragma unroll
+		for (int r = 0; r < R; ++r)
+			out[g * R + r] = base[g * R + r] + acc[r];
+	}
+};
+
 // Virtual row space [wq | wk | wv]; a wave owns the RoPE pair (2g, 2g+1).
 template <class WT>
 struct PQKV {

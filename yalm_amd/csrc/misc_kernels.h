@@ -49,7 +49,8 @@ __global__ __launch_bounds__(256) void step_begin_kernel(StepState *st, const vo
 // Greedy sampling on the device (sampler.cpp:27-38: strict '>' scan, so the
 // FIRST maximum wins). Feeds the result back as the next step's token.
 __global__ __launch_bounds__(1024) void argmax_kernel(const float *__restrict__ logits, int n, StepState *st,
-                                                      int *__restrict__ tokens_out, int cap) {
+                                                      int *__restrict__ tokens_out, int cap,
+                                                      float *__restrict__ pair_out = nullptr, int index_offset = 0) {
 	__shared__ float sv[16];
 	__shared__ int si[16];
 	float best = -FLT_MAX;
@@ -112,6 +113,11 @@ __global__ __launch_bounds__(1024) void argmax_kernel(const float *__restrict__ 
 		}
 		if (idx == 0x7fffffff)
 			idx = 0; // all -FLT_MAX / NaN: the reference returns 0
+		if (pair_out) { // tensor-parallel shard: publish (value, global index) for argmax_pick_kernel
+			pair_out[0] = b;
+			pair_out[1] = __int_as_float(idx + index_offset);
+			return;
+		}
 		const int k = st->n_gen;
 		if (tokens_out && k < cap)
 			tokens_out[k] = idx;
@@ -119,6 +125,29 @@ __global__ __launch_bounds__(1024) void argmax_kernel(const float *__restrict__ 
 		st->token = idx;
 		st->pos = st->pos + 1;
 	}
+}
+
+// Tensor parallelism: pick the global first maximum from the tp_size gathered
+// (value, index) pairs (ranks own ascending vocab slices, so ties resolve to the
+// lowest index as in sampler.cpp:27-38) and advance the step like argmax_kernel.
+__global__ void argmax_pick_kernel(const float *__restrict__ pairs, int n_pairs, StepState *st,
+                                   int *__restrict__ tokens_out, int cap) {
+	float b = pairs[0];
+	int idx = __float_as_int(pairs[1]);
+	for (int i = 1; i < n_pairs; ++i) {
+		const float v = pairs[2 * i];
+		const int j = __float_as_int(pairs[2 * i + 1]);
+		if (v > b || (v == b && j < idx)) {
+			b = v;
+			idx = j;
+		}
+	}
+	const int k = st->n_gen;
+	if (tokens_out && k < cap)
+		tokens_out[k] = idx;
+	st->n_gen = k + 1;
+	st->token = idx;
+	st->pos = st->pos + 1;
 }
 
 // Deterministic synthetic initialiser — the same integer hash as the CPU

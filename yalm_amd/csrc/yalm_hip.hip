@@ -6,6 +6,7 @@
 #include "../../include/yalm_hip.h"
 
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <cmath>
 #include <cstdio>
@@ -353,6 +354,45 @@ static int launch_attn(int head_dim, int n_heads, int n_kv, const float *q, cons
 	return YALM_OK;
 }
 
+// x += W v (fused_matmul_add_residuals). Under tensor parallelism W holds this
+// rank's input columns: rank 0 writes xs = x + W v, the others xs = W v, and
+// one RCCL all-reduce (sum, captured in the graph) lands x + sum_r W_r v_r in x
+// on every rank (identical bits on all ranks).
+template <class WT>
+static int enqueue_residual_gemv(yalm_decoder_s *d, const void *W, int n, const float *v, int kind) {
+	const yalm_config &c = d->c;
+	hipStream_t st = d->stream;
+	if (!d->comm) {
+		PResidual<WT, 1> p;
+		p.W = (const char *)W;
+		p.n = n;
+		p.out = d->x;
+		p.n_groups = c.dim;
+		return launch_gemv<WT, PResidual<WT, 1>, false>(p, v, nullptr, 0.f, kind, d->gemv[kind], st);
+	}
+	if (d->tp_rank == 0) {
+		PAddTo<WT, 1> p;
+		p.W = (const char *)W;
+		p.n = n;
+		p.out = d->xs;
+		p.base = d->x;
+		p.n_groups = c.dim;
+		TRY((launch_gemv<WT, PAddTo<WT, 1>, false>(p, v, nullptr, 0.f, kind, d->gemv[kind], st)));
+	} else {
+		PStore<WT, 1> p;
+		p.W = (const char *)W;
+		p.n = n;
+		p.out = d->xs;
+		p.n_groups = c.dim;
+		TRY((launch_gemv<WT, PStore<WT, 1>, false>(p, v, nullptr, 0.f, kind, d->gemv[kind], st)));
+	}
+	if (ncclAllReduce(d->xs, d->x, c.dim, ncclFloat, ncclSum, (ncclComm_t)d->comm, st) != ncclSuccess) {
+		set_err("ncclAllReduce failed");
+		return YALM_ERR_HIP;
+	}
+	return YALM_OK;
+}
+
 template <class WT>
 static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 	const yalm_config &c = d->c;
@@ -381,14 +421,8 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 	if (!(ab & 2))
 		TRY(launch_attn(c.head_dim, c.n_heads, c.n_kv_heads, d->q, w.key_cache, w.value_cache, d->step,
 		                c.max_seq_len, d->part, d->attn_counters, nullptr, d->xb2, st));
-	if (!(ab & 4)) {
-		PResidual<WT, 1> p;
-		p.W = (const char *)w.wo;
-		p.n = q_dim;
-		p.out = d->x;
-		p.n_groups = c.dim;
-		TRY((launch_gemv<WT, PResidual<WT, 1>, false>(p, d->xb2, nullptr, 0.f, GK_WO, d->gemv[GK_WO], st)));
-	}
+	if (!(ab & 4))
+		TRY(enqueue_residual_gemv<WT>(d, w.wo, q_dim, d->xb2, GK_WO));
 	if (ab & 8) {
 	} else if (c.act == YALM_SILU) {
 		PGlu<WT, 1> p;
@@ -407,14 +441,8 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 		p.n_groups = c.hidden_dim;
 		TRY((launch_gemv<WT, PGlu<WT, 0>, true>(p, d->x, w.rms_ffn, c.norm_eps, GK_GLU, d->gemv[GK_GLU], st)));
 	}
-	if (!(ab & 16)) {
-		PResidual<WT, 1> p;
-		p.W = (const char *)w.w2;
-		p.n = c.hidden_dim;
-		p.out = d->x;
-		p.n_groups = c.dim;
-		TRY((launch_gemv<WT, PResidual<WT, 1>, false>(p, d->hb, nullptr, 0.f, GK_W2, d->gemv[GK_W2], st)));
-	}
+	if (!(ab & 16))
+		TRY(enqueue_residual_gemv<WT>(d, w.w2, c.hidden_dim, d->hb, GK_W2));
 	return YALM_OK;
 }
 
@@ -425,14 +453,14 @@ static int enqueue_logits_t(yalm_decoder_s *d) {
 		PStore<WT, 2> p;
 		p.W = (const char *)d->wcls;
 		p.n = c.dim;
-		p.out = d->logits;
+		p.out = d->logits_local;
 		p.n_groups = c.vocab_size / 2;
 		return launch_gemv<WT, PStore<WT, 2>, true>(p, d->x, d->rms_final, c.norm_eps, GK_CLS, d->gemv[GK_CLS], d->stream);
 	}
 	PStore<WT, 1> p;
 	p.W = (const char *)d->wcls;
 	p.n = c.dim;
-	p.out = d->logits;
+	p.out = d->logits_local;
 	p.n_groups = c.vocab_size;
 	return launch_gemv<WT, PStore<WT, 1>, true>(p, d->x, d->rms_final, c.norm_eps, GK_CLS, d->gemv[GK_CLS], d->stream);
 }
@@ -457,10 +485,25 @@ static int enqueue_forward(yalm_decoder_s *d, int which) {
 		return YALM_OK;
 	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_logits_t, d));
 	if (which == GRAPH_LOGITS) {
-		HIPCHK(hipMemcpyAsync(d->logits_pinned, d->logits, sizeof(float) * d->c.vocab_size, hipMemcpyDeviceToHost,
+		if (d->comm && ncclAllGather(d->logits_local, d->logits, d->c.vocab_size, ncclFloat, (ncclComm_t)d->comm,
+		                             d->stream) != ncclSuccess) {
+			set_err("ncclAllGather (logits) failed");
+			return YALM_ERR_HIP;
+		}
+		HIPCHK(hipMemcpyAsync(d->logits_pinned, d->logits, sizeof(float) * d->vocab_full, hipMemcpyDeviceToHost,
 		                      d->stream));
-	} else {
+	} else if (!d->comm) {
 		argmax_kernel<<<1, 1024, 0, d->stream>>>(d->logits, d->c.vocab_size, d->step, d->tokens, d->tokens_cap);
+		HIPCHK(hipGetLastError());
+	} else { // sharded vocabulary: local first-max, gather (value, index) pairs, pick (identical on all ranks)
+		argmax_kernel<<<1, 1024, 0, d->stream>>>(d->logits_local, d->c.vocab_size, d->step, d->tokens,
+		                                         d->tokens_cap, d->amax, d->tp_rank * d->c.vocab_size);
+		HIPCHK(hipGetLastError());
+		if (ncclAllGather(d->amax, d->amax_all, 2, ncclFloat, (ncclComm_t)d->comm, d->stream) != ncclSuccess) {
+			set_err("ncclAllGather (argmax) failed");
+			return YALM_ERR_HIP;
+		}
+		argmax_pick_kernel<<<1, 1, 0, d->stream>>>(d->amax_all, d->tp_size, d->step, d->tokens, d->tokens_cap);
 		HIPCHK(hipGetLastError());
 	}
 	return YALM_OK;
@@ -505,6 +548,8 @@ static void destroy_decoder(yalm_decoder_s *d) {
 		if (d->graph[i])
 			(void)hipGraphDestroy(d->graph[i]);
 	}
+	if (d->comm)
+		(void)ncclCommDestroy((ncclComm_t)d->comm);
 	for (void *p : d->dev_allocs)
 		(void)hipFree(p);
 	if (d->logits_pinned)
@@ -532,12 +577,18 @@ static int replay(yalm_decoder_s *d, int which) {
 	return YALM_OK;
 }
 
-extern "C" int yalm_decoder_create(const yalm_config *config, const yalm_model_weights *weights, yalm_stream s,
-                                   yalm_decoder *out) {
+// comm: an initialised ncclComm_t (tensor parallelism) or null. config holds
+// the local (per-rank) dims; vocab_full the unsharded vocabulary.
+static int create_decoder(const yalm_config *config, const yalm_model_weights *weights, yalm_stream s,
+                          yalm_decoder *out, void *comm, int tp_rank, int tp_size, int vocab_full) {
 	ARGCHK(config && weights && out && weights->blocks, "yalm_decoder_create: null argument");
 	TRY(validate_config(config));
 	yalm_decoder_s *d = new yalm_decoder_s();
 	d->c = *config;
+	d->comm = comm;
+	d->tp_rank = tp_rank;
+	d->tp_size = tp_size;
+	d->vocab_full = vocab_full;
 	d->emb = weights->token_embedding;
 	d->rms_final = weights->rms_final;
 	d->wcls = weights->wcls;
@@ -569,7 +620,10 @@ extern "C" int yalm_decoder_create(const yalm_config *config, const yalm_model_w
 	    (r = dalloc(d, (void **)&d->hb, sizeof(float) * c.hidden_dim)) ||
 	    (r = dalloc(d, (void **)&d->part, sizeof(float) * (size_t)c.n_heads * nsplit * (c.head_dim + 2))) ||
 	    (r = dalloc(d, (void **)&d->attn_counters, sizeof(unsigned) * c.n_kv_heads)) ||
-	    (r = dalloc(d, (void **)&d->logits, sizeof(float) * c.vocab_size)) ||
+	    (r = dalloc(d, (void **)&d->logits, sizeof(float) * vocab_full)) ||
+	    (r = dalloc(d, (void **)&d->xs, sizeof(float) * c.dim)) ||
+	    (r = dalloc(d, (void **)&d->amax, sizeof(float) * 2)) ||
+	    (r = dalloc(d, (void **)&d->amax_all, sizeof(float) * 2 * tp_size)) ||
 	    (r = dalloc(d, (void **)&d->inv_freq, sizeof(float) * c.head_dim / 2)) ||
 	    (r = dalloc(d, (void **)&d->tokens, sizeof(int) * d->tokens_cap)))
 		return fail(r);
@@ -589,7 +643,10 @@ extern "C" int yalm_decoder_create(const yalm_config *config, const yalm_model_w
 		if (!bw.value_cache && (r = dalloc(d, (void **)&bw.value_cache, kvb)))
 			return fail(r);
 	}
-	if (hipHostMalloc((void **)&d->logits_pinned, sizeof(float) * c.vocab_size, hipHostMallocDefault) != hipSuccess) {
+	d->logits_local = d->logits;
+	if (comm && tp_size > 1 && (r = dalloc(d, (void **)&d->logits_local, sizeof(float) * c.vocab_size)))
+		return fail(r);
+	if (hipHostMalloc((void **)&d->logits_pinned, sizeof(float) * vocab_full, hipHostMallocDefault) != hipSuccess) {
 		set_err("hipHostMalloc failed");
 		return fail(YALM_ERR_HIP);
 	}
@@ -598,6 +655,57 @@ extern "C" int yalm_decoder_create(const yalm_config *config, const yalm_model_w
 		return fail(YALM_ERR_HIP);
 	}
 	*out = d;
+	return YALM_OK;
+}
+
+extern "C" int yalm_decoder_create(const yalm_config *config, const yalm_model_weights *weights, yalm_stream s,
+                                   yalm_decoder *out) {
+	ARGCHK(config, "yalm_decoder_create: null config");
+	return create_decoder(config, weights, s, out, nullptr, 0, 1, config->vocab_size);
+}
+
+// ------------------------------------------------------------------ tensor parallelism
+extern "C" int yalm_tp_unique_id(void *id_out) {
+	ARGCHK(id_out, "null id");
+	ncclUniqueId id;
+	if (ncclGetUniqueId(&id) != ncclSuccess) {
+		set_err("ncclGetUniqueId failed");
+		return YALM_ERR_HIP;
+	}
+	memcpy(id_out, &id, sizeof(id));
+	return YALM_OK;
+}
+
+extern "C" int yalm_decoder_create_tp(const yalm_config *config, const yalm_model_weights *weights, int tp_rank,
+                                      int tp_size, const void *unique_id, yalm_stream s, yalm_decoder *out) {
+	ARGCHK(config && weights && unique_id && out, "yalm_decoder_create_tp: null argument");
+	ARGCHK(tp_size >= 1 && tp_rank >= 0 && tp_rank < tp_size, "yalm_decoder_create_tp: bad rank / size");
+	const yalm_config &f = *config;
+	ARGCHK(f.n_kv_heads % tp_size == 0 && f.n_heads % tp_size == 0 && f.hidden_dim % tp_size == 0 &&
+	           f.vocab_size % tp_size == 0,
+	       "yalm_decoder_create_tp: n_heads, n_kv_heads, hidden_dim and vocab_size must divide by tp_size");
+	yalm_config lc = f;
+	lc.n_heads = f.n_heads / tp_size;
+	lc.n_kv_heads = f.n_kv_heads / tp_size;
+	lc.hidden_dim = f.hidden_dim / tp_size;
+	lc.vocab_size = f.vocab_size / tp_size;
+	ncclUniqueId id;
+	memcpy(&id, unique_id, sizeof(id));
+	ncclComm_t comm = nullptr;
+	if (ncclCommInitRank(&comm, tp_size, id, tp_rank) != ncclSuccess) {
+		set_err("ncclCommInitRank failed");
+		return YALM_ERR_HIP;
+	}
+	const int r = create_decoder(&lc, weights, s, out, comm, tp_rank, tp_size, f.vocab_size);
+	if (r != YALM_OK)
+		(void)ncclCommDestroy(comm);
+	return r;
+}
+
+extern "C" int yalm_copy_2d(void *dst, size_t dst_pitch, const void *src, size_t src_pitch, size_t width,
+                            size_t height) {
+	ARGCHK(dst && src && width <= dst_pitch && width <= src_pitch, "yalm_copy_2d: bad argument");
+	HIPCHK(hipMemcpy2D(dst, dst_pitch, src, src_pitch, width, height, hipMemcpyDeviceToDevice));
 	return YALM_OK;
 }
 
@@ -611,7 +719,7 @@ extern "C" int yalm_decoder_destroy(yalm_decoder d) {
 
 extern "C" int yalm_forward(yalm_decoder d, int token, int pos, int mode, float *logits_host) {
 	ARGCHK(d, "null decoder");
-	ARGCHK(token >= 0 && token < d->c.vocab_size, "token out of range");
+	ARGCHK(token >= 0 && token < d->vocab_full, "token out of range");
 	ARGCHK(pos >= 0, "negative pos");
 	const int which = mode == YALM_HYDRATE_KV_CACHE ? GRAPH_HYDRATE : GRAPH_LOGITS;
 	TRY(ensure_graph(d, which));
@@ -621,7 +729,7 @@ extern "C" int yalm_forward(yalm_decoder d, int token, int pos, int mode, float 
 	if (which == GRAPH_LOGITS) {
 		HIPCHK(hipStreamSynchronize(d->stream));
 		if (logits_host)
-			memcpy(logits_host, d->logits_pinned, sizeof(float) * d->c.vocab_size);
+			memcpy(logits_host, d->logits_pinned, sizeof(float) * d->vocab_full);
 	}
 	return YALM_OK;
 }
@@ -636,7 +744,7 @@ extern "C" int yalm_enqueue_greedy(yalm_decoder d, int n_steps) {
 
 extern "C" int yalm_generate_greedy(yalm_decoder d, int token, int pos, int n_steps, int *out_tokens) {
 	ARGCHK(d && out_tokens, "null argument");
-	ARGCHK(token >= 0 && token < d->c.vocab_size && pos >= 0 && n_steps >= 0, "bad token/pos/n_steps");
+	ARGCHK(token >= 0 && token < d->vocab_full && pos >= 0 && n_steps >= 0, "bad token/pos/n_steps");
 	TRY(ensure_graph(d, GRAPH_GREEDY));
 	int done = 0;
 	bool first = true;
@@ -697,7 +805,7 @@ extern "C" int yalm_set_x(yalm_decoder d, const float *host) {
 extern "C" int yalm_get_logits(yalm_decoder d, float *host) {
 	ARGCHK(d && host, "null argument");
 	HIPCHK(hipStreamSynchronize(d->stream));
-	HIPCHK(hipMemcpy(host, d->logits, sizeof(float) * d->c.vocab_size, hipMemcpyDeviceToHost));
+	HIPCHK(hipMemcpy(host, d->logits, sizeof(float) * d->vocab_full, hipMemcpyDeviceToHost));
 	return YALM_OK;
 }
 

@@ -181,6 +181,50 @@ def tensor_shapes(c: ModelConfig) -> dict:
     return out
 
 
+# ---- tensor parallelism (include/yalm_hip.h "tensor parallelism") ----
+def tp_shard(c: ModelConfig, name: str, rank: int, size: int):
+    """Megatron split of one .yalm tensor for rank/size: ("rows"|"cols", start,
+    count) of its [out][in] matrix, or None when replicated (norms, embedding).
+    The classifier ("model.output.weight", or the tied embedding used as
+    wcls) is split by vocabulary rows."""
+    if size == 1:
+        return None
+    if name in ("model.output.weight", "tp.wcls"):
+        n = c.vocab_size // size
+        return ("rows", rank * n, n)
+    kind = name.rsplit(".", 2)[-2] if name.startswith("model.layers.") else None
+    if kind in ("wq",):
+        n = c.q_dim // size
+        return ("rows", rank * n, n)
+    if kind in ("wk", "wv"):
+        n = c.kv_dim // size
+        return ("rows", rank * n, n)
+    if kind == "wo":
+        n = c.q_dim // size
+        return ("cols", rank * n, n)
+    if kind in ("w1", "w3"):
+        n = c.hidden_dim // size
+        return ("rows", rank * n, n)
+    if kind == "w2":
+        n = c.hidden_dim // size
+        return ("cols", rank * n, n)
+    return None
+
+
+def tp_check(c: ModelConfig, size: int) -> None:
+    if c.n_heads % size or c.n_kv_heads % size or c.hidden_dim % size or c.vocab_size % size:
+        raise ValueError(f"tensor parallel size {size} must divide n_heads, n_kv_heads, hidden_dim and vocab_size")
+
+
+def shard_array(c: ModelConfig, name: str, a, rank: int, size: int):
+    """Host-side slice of a full tensor (numpy) for rank/size."""
+    sh = tp_shard(c, name, rank, size)
+    if sh is None:
+        return a
+    kind, start, n = sh
+    return a[start:start + n] if kind == "rows" else a[:, start:start + n]
+
+
 # ---- deterministic synthetic init (same hash on device and in the oracle) ----
 WEIGHT_SCALE = 0.035  # uniform [-a, a): std 0.02, the usual init scale
 NORM_SCALE, NORM_OFFSET = 0.2, 1.0

@@ -108,6 +108,9 @@ _sig("yalm_matmul", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int])
 _sig("yalm_mha", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int])
 _sig("yalm_ffn", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int])
 _sig("yalm_prefill", c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p])
+_sig("yalm_tp_unique_id", c_int, [c_void_p])
+_sig("yalm_decoder_create_tp", c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p])
+_sig("yalm_copy_2d", c_int, [c_void_p, ctypes.c_size_t, c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t])
 _sig("yalm_prefill_time", c_int, [c_void_p, c_int, c_int, ctypes.POINTER(c_float)])
 _sig("yalm_gemm_f16", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int])
 _sig("yalm_attn_prefill", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int])
@@ -118,7 +121,8 @@ EXPORTED = [
     "yalm_synth", "yalm_decoder_create", "yalm_decoder_destroy", "yalm_forward", "yalm_generate_greedy",
     "yalm_enqueue_greedy", "yalm_device_step", "yalm_block", "yalm_get_x", "yalm_set_x", "yalm_get_logits",
     "yalm_time_kernel", "yalm_kernel_name", "yalm_set_gemv_config", "yalm_matmul", "yalm_mha", "yalm_ffn",
-    "yalm_prefill", "yalm_prefill_time", "yalm_gemm_f16", "yalm_attn_prefill",
+    "yalm_prefill", "yalm_prefill_time", "yalm_gemm_f16", "yalm_attn_prefill", "yalm_tp_unique_id",
+    "yalm_decoder_create_tp", "yalm_copy_2d",
 ]
 
 HYDRATE_KV_CACHE, OUTPUT_LOGITS = 0, 1
@@ -171,6 +175,13 @@ def ffn(x, w1, w2, w3, act: int, dtype: int) -> np.ndarray:
     return out
 
 
+def tp_unique_id() -> bytes:
+    """RCCL unique id for yalm_decoder_create_tp (rank 0 makes it, all ranks use it)."""
+    buf = ctypes.create_string_buffer(128)
+    check(lib.yalm_tp_unique_id(buf))
+    return buf.raw
+
+
 def gemm_f16(a: np.ndarray, w: np.ndarray) -> np.ndarray:
     """MFMA GEMM of the prefill path: a (M, K) f16 @ w (N, K)^T f16 -> (M, N) f32."""
     a = np.ascontiguousarray(a, dtype=np.float16)
@@ -201,6 +212,7 @@ class DeviceModel:
         self.cfg = cfg
         self.ptrs: dict = {}
         self._owned: list = []
+        self.tp = (0, 1)
 
     def _alloc(self, nbytes: int) -> int:
         p = lib.yalm_alloc(nbytes)
@@ -210,11 +222,18 @@ class DeviceModel:
         return p
 
     @classmethod
-    def from_arrays(cls, cfg: M.ModelConfig, tensors: dict) -> "DeviceModel":
-        """Upload host tensors (numpy; names as in .yalm)."""
+    def from_arrays(cls, cfg: M.ModelConfig, tensors: dict, tp=(0, 1)) -> "DeviceModel":
+        """Upload host tensors (numpy; names as in .yalm). tp = (rank, size):
+        upload only this rank's shards (models.tp_shard)."""
+        rank, size = tp
+        M.tp_check(cfg, size)
         self = cls(cfg)
-        for name, (shape, is_norm) in M.tensor_shapes(cfg).items():
-            a = np.ascontiguousarray(tensors[name])
+        self.tp = tp
+        items = dict(tensors)
+        if size > 1 and cfg.tied:
+            items["tp.wcls"] = tensors["model.embed.weight"]
+        for name in list(M.tensor_shapes(cfg)) + (["tp.wcls"] if size > 1 and cfg.tied else []):
+            a = np.ascontiguousarray(M.shard_array(cfg, name, items[name], rank, size))
             p = lib.yalm_upload(a.ctypes.data, a.nbytes)
             if not p:
                 raise YalmError(lib.yalm_last_error().decode())
@@ -237,16 +256,46 @@ class DeviceModel:
             yd.close()
 
     @classmethod
-    def synthetic(cls, cfg: M.ModelConfig, seed: int = 1) -> "DeviceModel":
+    def synthetic(cls, cfg: M.ModelConfig, seed: int = 1, tp=(0, 1)) -> "DeviceModel":
         """Random-weight model of cfg's shape generated directly in HBM with the
-        deterministic hash shared with the oracle (no PCIe upload)."""
+        deterministic hash shared with the oracle (no PCIe upload). tp = (rank,
+        size): keep only this rank's shards — each sharded tensor is generated
+        whole in a scratch buffer and its slice copied out (yalm_copy_2d), so
+        every rank holds exactly the slices of the same full model."""
+        rank, size = tp
+        M.tp_check(cfg, size)
         self = cls(cfg)
-        for name, (shape, is_norm) in M.tensor_shapes(cfg).items():
+        self.tp = tp
+        names = list(M.tensor_shapes(cfg).items())
+        if size > 1 and cfg.tied:
+            names.append(("tp.wcls", ((cfg.vocab_size, cfg.dim), False)))
+        for name, (shape, is_norm) in names:
             n = int(np.prod(shape))
             dt = M.F32 if is_norm else cfg.weight_dtype
-            p = self._alloc(n * M.DTYPE_BYTES[dt])
-            scale, offset = M.synth_params(name, is_norm)
-            check(lib.yalm_synth(p, n, dt, M.synth_seed(seed, name), scale, offset, None))
+            eb = M.DTYPE_BYTES[dt]
+            src_name = "model.embed.weight" if name == "tp.wcls" else name
+            scale, offset = M.synth_params(src_name, is_norm)
+            sh = M.tp_shard(cfg, name, rank, size)
+            if sh is None:
+                p = self._alloc(n * eb)
+                check(lib.yalm_synth(p, n, dt, M.synth_seed(seed, src_name), scale, offset, None))
+            else:
+                full = lib.yalm_alloc(n * eb)
+                if not full:
+                    raise YalmError(lib.yalm_last_error().decode())
+                try:
+                    check(lib.yalm_synth(full, n, dt, M.synth_seed(seed, src_name), scale, offset, None))
+                    kind, start, cnt = sh
+                    rows, cols = shape
+                    if kind == "rows":
+                        p = self._alloc(cnt * cols * eb)
+                        check(lib.yalm_copy_2d(p, cols * eb, full + start * cols * eb, cols * eb, cols * eb, cnt))
+                    else:
+                        p = self._alloc(rows * cnt * eb)
+                        check(lib.yalm_copy_2d(p, cnt * eb, full + start * eb, cols * eb, cnt * eb, rows))
+                finally:
+                    check(lib.yalm_stream_sync(None))
+                    lib.yalm_free(full)
             self.ptrs[name] = p
         check(lib.yalm_stream_sync(None))
         return self
@@ -259,7 +308,7 @@ class DeviceModel:
             for k, name in n.items():
                 setattr(blocks[l], k, self.ptrs[name])
         emb = self.ptrs["model.embed.weight"]
-        wcls = self.ptrs.get("model.output.weight", emb)
+        wcls = self.ptrs.get("model.output.weight", self.ptrs.get("tp.wcls", emb))
         mw = ModelWeights(emb, self.ptrs["model.norm.weight"], wcls, blocks)
         return mw, blocks
 
@@ -273,14 +322,23 @@ class DeviceModel:
 class Decoder:
     """InferenceState on the device + Model::forward (graph-replayed)."""
 
-    def __init__(self, model: DeviceModel):
+    def __init__(self, model: DeviceModel, tp_id: bytes = None):
+        """tp_id: the RCCL unique id (tp_unique_id() on rank 0, shared with the
+        other ranks) for a tensor-parallel decoder over model.tp = (rank, size);
+        None for a single-GPU decoder."""
         self.model = model
         self.cfg = model.cfg
         self._c = Config.from_model(self.cfg)
         mw, self._blocks = model.weights_struct()
         self._mw = mw
         h = c_void_p()
-        check(lib.yalm_decoder_create(ctypes.byref(self._c), ctypes.byref(mw), None, ctypes.byref(h)))
+        if tp_id is None:
+            check(lib.yalm_decoder_create(ctypes.byref(self._c), ctypes.byref(mw), None, ctypes.byref(h)))
+        else:
+            rank, size = getattr(model, "tp", (0, 1))
+            idb = ctypes.create_string_buffer(bytes(tp_id), 128)
+            check(lib.yalm_decoder_create_tp(ctypes.byref(self._c), ctypes.byref(mw), rank, size, idb, None,
+                                             ctypes.byref(h)))
         self.h = h
 
     def forward(self, token: int, pos: int, mode: int = OUTPUT_LOGITS):
