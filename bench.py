@@ -37,7 +37,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample budget")
     ap.add_argument("--kernel-iters", type=int, default=64)
     ap.add_argument("--tp", action="store_true",
-                    help="tensor parallel over the launched ranks (one sequence, RCCL all-reduce) instead of replicas")
+                    help="tensor parallel over the launched ranks (one sequence) instead of replicas")
+    ap.add_argument("--tp-transport", default="rccl", choices=["rccl", "ipc"],
+                    help="all-reduce transport for --tp: RCCL (one rank per GPU) or the IPC one-shot exchange")
     return ap.parse_args()
 
 
@@ -132,10 +134,20 @@ def main():
     if args.tp:
         # one sequence sharded over all ranks (Megatron split, RCCL all-reduce in the graph)
         dm = runtime.DeviceModel.synthetic(cfg, seed=1, tp=(rank, world))
-        uid = [runtime.tp_unique_id() if rank == 0 else None]
-        if dist is not None:
-            dist.broadcast_object_list(uid, src=0)
-        dec = runtime.Decoder(dm, tp_id=uid[0])
+        if args.tp_transport == "ipc":
+            def gather(h):
+                if dist is None:
+                    return [h]
+                out = [None] * world
+                dist.all_gather_object(out, h)
+                return out
+
+            dec = runtime.Decoder(dm, tp_gather=gather)
+        else:
+            uid = [runtime.tp_unique_id() if rank == 0 else None]
+            if dist is not None:
+                dist.broadcast_object_list(uid, src=0)
+            dec = runtime.Decoder(dm, tp_id=uid[0])
     else:
         dm = runtime.DeviceModel.synthetic(cfg, seed=1)
         dec = runtime.Decoder(dm)
@@ -217,7 +229,8 @@ def main():
             "model": args.model,
             "global_batch": world,
             "seq_len": int(pos1),
-            "parallelism": (f"tp{world}" if args.tp else f"replicas{world}") if world > 1 else ("tp1" if args.tp else "single"),
+            "parallelism": (f"tp{world}-{args.tp_transport}" if args.tp else
+                            (f"replicas{world}" if world > 1 else "single")),
         },
         "step_roofline": {
             "bytes_per_token": int(bytes_per_tok),

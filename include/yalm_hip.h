@@ -167,6 +167,18 @@ int yalm_tp_unique_id(void *id_out);
  * logits (full vocabulary) and greedy tokens are identical on all ranks. */
 int yalm_decoder_create_tp(const yalm_config *config, const yalm_model_weights *weights, int tp_rank, int tp_size,
                            const void *unique_id, yalm_stream s, yalm_decoder *out);
+/* The same split with an IPC one-shot exchange instead of RCCL (no NCCL
+ * communicator; also runs several ranks on ONE GPU, which RCCL refuses): each
+ * rank allocates its exchange buffer (yalm_tp_ipc_alloc, config = full model)
+ * and shares the 64-byte hipIpcMemHandle out of band; every rank then passes
+ * all tp_size handles (rank order; its own entry is ignored). The decoder
+ * takes ownership of own_buf. Per exchange: the producer GEMV writes this
+ * rank's partial into a slot of its buffer, then one kernel signals every peer
+ * (system-scope flag stores), waits for theirs and sums (or gathers) all
+ * ranks' slots in rank order, so results are identical on every rank. */
+int yalm_tp_ipc_alloc(const yalm_config *config, int tp_size, void **buf, void *handle_out);
+int yalm_decoder_create_tp_ipc(const yalm_config *config, const yalm_model_weights *weights, int tp_rank, int tp_size,
+                               void *own_buf, const void *handles, yalm_stream s, yalm_decoder *out);
 /* Device-to-device 2D copy (hipMemcpy2D): shard slicing of weights resident in HBM. */
 int yalm_copy_2d(void *dst, size_t dst_pitch, const void *src, size_t src_pitch, size_t width, size_t height);
 

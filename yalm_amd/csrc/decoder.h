@@ -98,5 +98,12 @@ struct yalm_decoder_s {
 	float *logits_local = nullptr;   // [vocab / tp] this rank's logits rows (== logits without TP)
 	float *amax = nullptr;           // [2] local argmax (value, global index as float bits)
 	float *amax_all = nullptr;       // [2 * tp_size]
+	// IPC one-shot exchange transport (yalm_decoder_create_tp_ipc): every rank's
+	// buffer [2 slots x ipc_S floats][flags: 64 u32][seq u32] mapped on all ranks
+	bool ipc = false;
+	int ipc_S = 0;                   // floats per slot
+	float *ipc_own = nullptr;        // this rank's buffer
+	float **ipc_bufs = nullptr;      // device array [tp_size] of buffer bases (peers opened via IPC)
+	std::vector<void *> ipc_opened;  // hipIpcOpenMemHandle mappings to close
 };
 

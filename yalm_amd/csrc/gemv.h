@@ -92,6 +92,39 @@ struct PAddTo {
 	}
 };
 
+// IPC tensor-parallel partial: out = slot buffer chosen at run time by the
+// exchange sequence number (slot (seq + 1) & 1 of this rank's IPC buffer, so
+// consecutive exchanges alternate slots whatever graph runs), rank 0 adding
+// the residual base (x) as PAddTo does.
+template <class WT, int R_>
+struct PSlot {
+	static constexpr int R = R_;
+	const char *W;
+	int n;
+	float *slots;        // this rank's IPC buffer
+	int S, offset;       // floats per slot, offset inside the slot
+	const unsigned *seq; // exchange sequence counter (in the IPC buffer)
+	const float *base;   // residual (rank 0) or null
+	int n_groups;
+	__device__ __forceinline__ void prologue() const {}
+	__device__ __forceinline__ const char *row(int g, int r) const {
+		return W + (size_t)(g * R + r) * n * WT::BYTES;
+	}
+	__device__ __forceinline__ float *out() const {
+		return slots + (size_t)((*seq + 1u) & 1u) * S + offset;
+	}
+	__device__ __forceinline__ void finish(int g, const float *acc, int lane) const {
+		if (lane < R)
+			out()[g * R + lane] = (base ? base[g * R + lane] : 0.0f) + acc[lane];
+	}
+	__device__ __forceinline__ void finish_all(int g, const float *acc) const {
+		float *o = out();
+#pragma unroll
+		for (int r = 0; r < R; ++r)
+			o[g * R + r] = (base ? base[g * R + r] : 0.0f) + acc[r];
+	}
+};
+
 // Virtual row space [wq | wk | wv]; a wave owns the RoPE pair (2g, 2g+1).
 template <class WT>
 struct PQKV {

@@ -50,7 +50,14 @@ __global__ __launch_bounds__(256) void step_begin_kernel(StepState *st, const vo
 // FIRST maximum wins). Feeds the result back as the next step's token.
 __global__ __launch_bounds__(1024) void argmax_kernel(const float *__restrict__ logits, int n, StepState *st,
                                                       int *__restrict__ tokens_out, int cap,
-                                                      float *__restrict__ pair_out = nullptr, int index_offset = 0) {
+                                                      float *__restrict__ pair_out = nullptr, int index_offset = 0,
+                                                      const unsigned *__restrict__ slot_seq = nullptr,
+                                                      int slot_floats = 0) {
+	if (slot_seq) { // IPC transport: logits and the pair live in slot (seq + 1) & 1
+		const size_t so = (size_t)((*slot_seq + 1u) & 1u) * slot_floats;
+		logits += so;
+		pair_out += so;
+	}
 	__shared__ float sv[16];
 	__shared__ int si[16];
 	float best = -FLT_MAX;
@@ -148,6 +155,64 @@ __global__ void argmax_pick_kernel(const float *__restrict__ pairs, int n_pairs,
 	st->n_gen = k + 1;
 	st->token = idx;
 	st->pos = st->pos + 1;
+}
+
+// One-shot exchange over IPC-mapped peer buffers (tensor parallelism without
+// RCCL; works with several ranks on one GPU). Each rank's buffer: two data
+// slots of S floats, 64 arrival flags (written by the peers), a sequence word.
+// Exchange k (seq = k + 1): the producer kernel already left this rank's data
+// in slot seq & 1; signal every peer (system-scope store of seq into its flag
+// [rank]), wait until every peer's flag here reaches seq (bounded), then
+//   SUM:    out[i] = sum over ranks p (in rank order) of slot_p[offset + i]
+//   GATHER: out[p * count + i] = slot_p[offset + i]
+// with system-scope loads. A slot is rewritten two exchanges later, after
+// every peer has signalled the exchange in between, i.e. finished reading it.
+enum { IPC_SUM = 0, IPC_GATHER = 1 };
+__global__ __launch_bounds__(1024) void ipc_exchange_kernel(float *const *__restrict__ bufs, int rank, int n_ranks,
+                                                            int S, int offset, int count, int mode,
+                                                            float *__restrict__ out) {
+	float *const own = bufs[rank];
+	unsigned *const flags = (unsigned *)(own + 2 * (size_t)S);
+	unsigned *const seqp = flags + 64;
+	const unsigned seq = *seqp + 1u; // only this rank's (stream-ordered) kernels write it
+	const size_t so = (size_t)(seq & 1u) * S + offset;
+	if (threadIdx.x == 0) {
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, ""); // this rank's slot data before the signal
+		for (int p = 0; p < n_ranks; ++p)
+			if (p != rank)
+				__hip_atomic_store((unsigned *)(bufs[p] + 2 * (size_t)S) + rank, seq, __ATOMIC_RELAXED,
+				                   __HIP_MEMORY_SCOPE_SYSTEM);
+		for (int p = 0; p < n_ranks; ++p) {
+			if (p == rank)
+				continue;
+			long spins = 0;
+			while ((int)(__hip_atomic_load(flags + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - seq) < 0) {
+				if (++spins > (1l << 24)) { // a peer never arrived: give up (results wrong, no hang)
+					__hip_atomic_store(flags + 63, 0xdeadu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+					break;
+				}
+				__builtin_amdgcn_s_sleep(2);
+			}
+		}
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+	}
+	__syncthreads();
+	if (mode == IPC_SUM) {
+		for (int i = threadIdx.x; i < count; i += blockDim.x) {
+			float s = 0.0f;
+			for (int p = 0; p < n_ranks; ++p)
+				s += __hip_atomic_load(bufs[p] + so + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+			out[i] = s;
+		}
+	} else {
+		for (int p = 0; p < n_ranks; ++p)
+			for (int i = threadIdx.x; i < count; i += blockDim.x)
+				out[(size_t)p * count + i] =
+				    __hip_atomic_load(bufs[p] + so + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+	}
+	__syncthreads();
+	if (threadIdx.x == 0)
+		*seqp = seq;
 }
 
 // Deterministic synthetic initialiser — the same integer hash as the CPU

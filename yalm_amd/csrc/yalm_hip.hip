@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -354,6 +355,10 @@ static int launch_attn(int head_dim, int n_heads, int n_kv, const float *q, cons
 	return YALM_OK;
 }
 
+static const unsigned *ipc_seq(const yalm_decoder_s *d) {
+	return (const unsigned *)(d->ipc_own + 2 * (size_t)d->ipc_S) + 64;
+}
+
 // x += W v (fused_matmul_add_residuals). Under tensor parallelism W holds this
 // rank's input columns: rank 0 writes xs = x + W v, the others xs = W v, and
 // one RCCL all-reduce (sum, captured in the graph) lands x + sum_r W_r v_r in x
@@ -362,6 +367,22 @@ template <class WT>
 static int enqueue_residual_gemv(yalm_decoder_s *d, const void *W, int n, const float *v, int kind) {
 	const yalm_config &c = d->c;
 	hipStream_t st = d->stream;
+	if (d->ipc) { // partial (+ x on rank 0) into this exchange's slot, then SUM over the ranks into x
+		PSlot<WT, 1> p;
+		p.W = (const char *)W;
+		p.n = n;
+		p.slots = d->ipc_own;
+		p.S = d->ipc_S;
+		p.offset = 0;
+		p.seq = ipc_seq(d);
+		p.base = d->tp_rank == 0 ? d->x : nullptr;
+		p.n_groups = c.dim;
+		TRY((launch_gemv<WT, PSlot<WT, 1>, false>(p, v, nullptr, 0.f, kind, d->gemv[kind], st)));
+		ipc_exchange_kernel<<<1, 1024, 0, st>>>(d->ipc_bufs, d->tp_rank, d->tp_size, d->ipc_S, 0, c.dim, IPC_SUM,
+		                                       d->x);
+		HIPCHK(hipGetLastError());
+		return YALM_OK;
+	}
 	if (!d->comm) {
 		PResidual<WT, 1> p;
 		p.W = (const char *)W;
@@ -449,6 +470,19 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 template <class WT>
 static int enqueue_logits_t(yalm_decoder_s *d) {
 	const yalm_config &c = d->c;
+	if (d->ipc) { // this rank's vocabulary rows into the exchange slot, after the 2-float argmax pair
+		PSlot<WT, 1> p;
+		p.W = (const char *)d->wcls;
+		p.n = c.dim;
+		p.slots = d->ipc_own;
+		p.S = d->ipc_S;
+		p.offset = 2;
+		p.seq = ipc_seq(d);
+		p.base = nullptr;
+		p.n_groups = c.vocab_size;
+		return launch_gemv<WT, PSlot<WT, 1>, true>(p, d->x, d->rms_final, c.norm_eps, GK_CLS, d->gemv[GK_CLS],
+		                                           d->stream);
+	}
 	if (c.vocab_size % 2 == 0) {
 		PStore<WT, 2> p;
 		p.W = (const char *)d->wcls;
@@ -484,6 +518,26 @@ static int enqueue_forward(yalm_decoder_s *d, int which) {
 	if (which == GRAPH_HYDRATE)
 		return YALM_OK;
 	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_logits_t, d));
+	if (d->ipc) {
+		if (which == GRAPH_LOGITS) {
+			ipc_exchange_kernel<<<1, 1024, 0, d->stream>>>(d->ipc_bufs, d->tp_rank, d->tp_size, d->ipc_S, 2,
+			                                              d->c.vocab_size, IPC_GATHER, d->logits);
+			HIPCHK(hipGetLastError());
+			HIPCHK(hipMemcpyAsync(d->logits_pinned, d->logits, sizeof(float) * d->vocab_full, hipMemcpyDeviceToHost,
+			                      d->stream));
+		} else {
+			argmax_kernel<<<1, 1024, 0, d->stream>>>(d->ipc_own + 2, d->c.vocab_size, d->step, d->tokens,
+			                                         d->tokens_cap, d->ipc_own, d->tp_rank * d->c.vocab_size,
+			                                         ipc_seq(d), d->ipc_S);
+			HIPCHK(hipGetLastError());
+			ipc_exchange_kernel<<<1, 1024, 0, d->stream>>>(d->ipc_bufs, d->tp_rank, d->tp_size, d->ipc_S, 0, 2,
+			                                              IPC_GATHER, d->amax_all);
+			HIPCHK(hipGetLastError());
+			argmax_pick_kernel<<<1, 1, 0, d->stream>>>(d->amax_all, d->tp_size, d->step, d->tokens, d->tokens_cap);
+			HIPCHK(hipGetLastError());
+		}
+		return YALM_OK;
+	}
 	if (which == GRAPH_LOGITS) {
 		if (d->comm && ncclAllGather(d->logits_local, d->logits, d->c.vocab_size, ncclFloat, (ncclComm_t)d->comm,
 		                             d->stream) != ncclSuccess) {
@@ -550,6 +604,10 @@ static void destroy_decoder(yalm_decoder_s *d) {
 	}
 	if (d->comm)
 		(void)ncclCommDestroy((ncclComm_t)d->comm);
+	for (void *p : d->ipc_opened)
+		(void)hipIpcCloseMemHandle(p);
+	if (d->ipc_own)
+		(void)hipFree(d->ipc_own);
 	for (void *p : d->dev_allocs)
 		(void)hipFree(p);
 	if (d->logits_pinned)
@@ -644,7 +702,7 @@ static int create_decoder(const yalm_config *config, const yalm_model_weights *w
 			return fail(r);
 	}
 	d->logits_local = d->logits;
-	if (comm && tp_size > 1 && (r = dalloc(d, (void **)&d->logits_local, sizeof(float) * c.vocab_size)))
+	if (tp_size > 1 && (r = dalloc(d, (void **)&d->logits_local, sizeof(float) * c.vocab_size)))
 		return fail(r);
 	if (hipHostMalloc((void **)&d->logits_pinned, sizeof(float) * vocab_full, hipHostMallocDefault) != hipSuccess) {
 		set_err("hipHostMalloc failed");
@@ -665,6 +723,23 @@ extern "C" int yalm_decoder_create(const yalm_config *config, const yalm_model_w
 }
 
 // ------------------------------------------------------------------ tensor parallelism
+static int tp_local_config(const yalm_config &f, int tp_size, yalm_config &lc) {
+	ARGCHK(f.n_kv_heads % tp_size == 0 && f.n_heads % tp_size == 0 && f.hidden_dim % tp_size == 0 &&
+	           f.vocab_size % tp_size == 0,
+	       "tensor parallel: n_heads, n_kv_heads, hidden_dim and vocab_size must divide by tp_size");
+	lc = f;
+	lc.n_heads = f.n_heads / tp_size;
+	lc.n_kv_heads = f.n_kv_heads / tp_size;
+	lc.hidden_dim = f.hidden_dim / tp_size;
+	lc.vocab_size = f.vocab_size / tp_size;
+	return YALM_OK;
+}
+
+static int ipc_slot_floats(const yalm_config &f, int tp_size) {
+	const int need = std::max(f.dim, f.vocab_size / tp_size + 2);
+	return (need + 63) / 64 * 64;
+}
+
 extern "C" int yalm_tp_unique_id(void *id_out) {
 	ARGCHK(id_out, "null id");
 	ncclUniqueId id;
@@ -681,14 +756,8 @@ extern "C" int yalm_decoder_create_tp(const yalm_config *config, const yalm_mode
 	ARGCHK(config && weights && unique_id && out, "yalm_decoder_create_tp: null argument");
 	ARGCHK(tp_size >= 1 && tp_rank >= 0 && tp_rank < tp_size, "yalm_decoder_create_tp: bad rank / size");
 	const yalm_config &f = *config;
-	ARGCHK(f.n_kv_heads % tp_size == 0 && f.n_heads % tp_size == 0 && f.hidden_dim % tp_size == 0 &&
-	           f.vocab_size % tp_size == 0,
-	       "yalm_decoder_create_tp: n_heads, n_kv_heads, hidden_dim and vocab_size must divide by tp_size");
-	yalm_config lc = f;
-	lc.n_heads = f.n_heads / tp_size;
-	lc.n_kv_heads = f.n_kv_heads / tp_size;
-	lc.hidden_dim = f.hidden_dim / tp_size;
-	lc.vocab_size = f.vocab_size / tp_size;
+	yalm_config lc;
+	TRY(tp_local_config(f, tp_size, lc));
 	ncclUniqueId id;
 	memcpy(&id, unique_id, sizeof(id));
 	ncclComm_t comm = nullptr;
@@ -700,6 +769,67 @@ extern "C" int yalm_decoder_create_tp(const yalm_config *config, const yalm_mode
 	if (r != YALM_OK)
 		(void)ncclCommDestroy(comm);
 	return r;
+}
+
+extern "C" int yalm_tp_ipc_alloc(const yalm_config *config, int tp_size, void **buf, void *handle_out) {
+	ARGCHK(config && buf && handle_out && tp_size >= 1 && tp_size <= 63, "yalm_tp_ipc_alloc: bad argument");
+	const size_t bytes = (2 * (size_t)ipc_slot_floats(*config, tp_size) + 128) * sizeof(float);
+	HIPCHK(hipMalloc(buf, bytes));
+	HIPCHK(hipMemset(*buf, 0, bytes));
+	hipIpcMemHandle_t h;
+	HIPCHK(hipIpcGetMemHandle(&h, *buf));
+	memcpy(handle_out, &h, sizeof(h));
+	HIPCHK(hipDeviceSynchronize());
+	return YALM_OK;
+}
+
+extern "C" int yalm_decoder_create_tp_ipc(const yalm_config *config, const yalm_model_weights *weights, int tp_rank,
+                                          int tp_size, void *own_buf, const void *handles, yalm_stream s,
+                                          yalm_decoder *out) {
+	ARGCHK(config && weights && own_buf && handles && out, "yalm_decoder_create_tp_ipc: null argument");
+	ARGCHK(tp_size >= 1 && tp_size <= 63 && tp_rank >= 0 && tp_rank < tp_size, "bad rank / size");
+	yalm_config lc;
+	TRY(tp_local_config(*config, tp_size, lc));
+	std::vector<float *> bases(tp_size);
+	std::vector<void *> opened;
+	for (int p = 0; p < tp_size; ++p) {
+		if (p == tp_rank) {
+			bases[p] = (float *)own_buf;
+			continue;
+		}
+		hipIpcMemHandle_t h;
+		memcpy(&h, (const char *)handles + (size_t)p * sizeof(h), sizeof(h));
+		void *ptr = nullptr;
+		if (hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+			for (void *q : opened)
+				(void)hipIpcCloseMemHandle(q);
+			set_err("hipIpcOpenMemHandle failed");
+			return YALM_ERR_HIP;
+		}
+		opened.push_back(ptr);
+		bases[p] = (float *)ptr;
+	}
+	const int r = create_decoder(&lc, weights, s, out, nullptr, tp_rank, tp_size, config->vocab_size);
+	if (r != YALM_OK) {
+		for (void *q : opened)
+			(void)hipIpcCloseMemHandle(q);
+		return r;
+	}
+	yalm_decoder_s *d = *out;
+	d->ipc = true;
+	d->ipc_S = ipc_slot_floats(*config, tp_size);
+	d->ipc_own = (float *)own_buf;
+	d->ipc_opened = opened;
+	void *dev_bases = nullptr;
+	if (dalloc(d, &dev_bases, sizeof(float *) * tp_size) != YALM_OK ||
+	    hipMemcpy(dev_bases, bases.data(), sizeof(float *) * tp_size, hipMemcpyHostToDevice) != hipSuccess) {
+		destroy_decoder(d);
+		*out = nullptr;
+		set_err("IPC pointer table upload failed");
+		return YALM_ERR_HIP;
+	}
+	d->ipc_bufs = (float **)dev_bases;
+	return YALM_OK;
 }
 
 extern "C" int yalm_copy_2d(void *dst, size_t dst_pitch, const void *src, size_t src_pitch, size_t width,

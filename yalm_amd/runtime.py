@@ -110,6 +110,8 @@ _sig("yalm_ffn", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int
 _sig("yalm_prefill", c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p])
 _sig("yalm_tp_unique_id", c_int, [c_void_p])
 _sig("yalm_decoder_create_tp", c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p])
+_sig("yalm_tp_ipc_alloc", c_int, [c_void_p, c_int, ctypes.POINTER(c_void_p), c_void_p])
+_sig("yalm_decoder_create_tp_ipc", c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p])
 _sig("yalm_copy_2d", c_int, [c_void_p, ctypes.c_size_t, c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t])
 _sig("yalm_prefill_time", c_int, [c_void_p, c_int, c_int, ctypes.POINTER(c_float)])
 _sig("yalm_gemm_f16", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int])
@@ -122,7 +124,7 @@ EXPORTED = [
     "yalm_enqueue_greedy", "yalm_device_step", "yalm_block", "yalm_get_x", "yalm_set_x", "yalm_get_logits",
     "yalm_time_kernel", "yalm_kernel_name", "yalm_set_gemv_config", "yalm_matmul", "yalm_mha", "yalm_ffn",
     "yalm_prefill", "yalm_prefill_time", "yalm_gemm_f16", "yalm_attn_prefill", "yalm_tp_unique_id",
-    "yalm_decoder_create_tp", "yalm_copy_2d",
+    "yalm_decoder_create_tp", "yalm_copy_2d", "yalm_tp_ipc_alloc", "yalm_decoder_create_tp_ipc",
 ]
 
 HYDRATE_KV_CACHE, OUTPUT_LOGITS = 0, 1
@@ -322,17 +324,30 @@ class DeviceModel:
 class Decoder:
     """InferenceState on the device + Model::forward (graph-replayed)."""
 
-    def __init__(self, model: DeviceModel, tp_id: bytes = None):
-        """tp_id: the RCCL unique id (tp_unique_id() on rank 0, shared with the
-        other ranks) for a tensor-parallel decoder over model.tp = (rank, size);
-        None for a single-GPU decoder."""
+    def __init__(self, model: DeviceModel, tp_id: bytes = None, tp_gather=None):
+        """Tensor parallel over model.tp = (rank, size), one of:
+        tp_id: the RCCL unique id (tp_unique_id() on rank 0, shared with the
+        other ranks); tp_gather: a function mapping this rank's 64-byte IPC
+        handle to the list of every rank's handle (e.g. via
+        torch.distributed.all_gather_object) for the IPC exchange transport.
+        Neither: a single-GPU decoder."""
         self.model = model
         self.cfg = model.cfg
         self._c = Config.from_model(self.cfg)
         mw, self._blocks = model.weights_struct()
         self._mw = mw
         h = c_void_p()
-        if tp_id is None:
+        if tp_gather is not None:
+            rank, size = getattr(model, "tp", (0, 1))
+            buf = c_void_p()
+            handle = ctypes.create_string_buffer(64)
+            check(lib.yalm_tp_ipc_alloc(ctypes.byref(self._c), size, ctypes.byref(buf), handle))
+            handles = tp_gather(handle.raw)
+            assert len(handles) == size and all(len(x) == 64 for x in handles)
+            hb = ctypes.create_string_buffer(b"".join(handles), 64 * size)
+            check(lib.yalm_decoder_create_tp_ipc(ctypes.byref(self._c), ctypes.byref(mw), rank, size, buf, hb, None,
+                                                 ctypes.byref(h)))
+        elif tp_id is None:
             check(lib.yalm_decoder_create(ctypes.byref(self._c), ctypes.byref(mw), None, ctypes.byref(h)))
         else:
             rank, size = getattr(model, "tp", (0, 1))
