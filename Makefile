@@ -33,4 +33,10 @@ clean:
 	$(MAKE) -C oracle clean
 	$(MAKE) -C yalm_amd/host clean
 
-.PHONY: all oracle host clean resource-usage
+# microbenchmarks (tools/*.hip -> tools/<name>; git-ignored binaries)
+TOOLS = stream_bench launch_bench persist_bench mall_bench concurrency_check wg_timeline
+tools: $(addprefix tools/,$(TOOLS))
+tools/%: tools/%.hip $(HIP_HDRS)
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
+
+.PHONY: all oracle host clean resource-usage tools
