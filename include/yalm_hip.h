@@ -135,7 +135,8 @@ int yalm_get_logits(yalm_decoder d, float *host);
 /* Average device time (ms) of one kernel of the forward, launched eagerly on
  * the decoder's stream `iters` times between HIP events. kernel_id: 0 = QKV
  * GEMV, 1 = attention, 2 = Wo GEMV, 3 = W1/W3 GEMV+GLU, 4 = W2 GEMV,
- * 5 = logits GEMV. Used by bench.py for the roofline of the dominant kernel. */
+ * 5 = logits GEMV, 6 = the whole-token engine launch (greedy mode; advances
+ * the decoder's device step). Used by bench.py for the roofline of the dominant kernel. */
 int yalm_time_kernel(yalm_decoder d, int kernel_id, int iters, float *avg_ms);
 /* Override the GEMV launch geometry of one weight-streaming kernel kind
  * (0 = QKV, 1 = Wo, 2 = W1/W3, 3 = W2, 4 = logits): workgroup size
@@ -144,8 +145,14 @@ int yalm_time_kernel(yalm_decoder d, int kernel_id, int iters, float *avg_ms);
  * kernel under YALM_GEMV_LEGACY=1); 0 = automatic.
  * Drops captured graphs (re-captured on next use). Tuning/ablation hook. */
 int yalm_set_gemv_config(yalm_decoder d, int kind, int threads, int unroll, int gpw);
-/* Name of kernel_id's device function (to match rocprofv3 summaries). */
+/* Name of kernel_id's device function (to match rocprofv3 summaries).
+ * kernel_id 6 = the persistent per-token engine (yalm_decoder_engine). */
 const char *yalm_kernel_name(yalm_decoder d, int kernel_id);
+/* 1 if this decoder runs each token as ONE persistent launch (engine.h: LDS-DMA
+ * weight ring + in-launch epoch seams), 0 if it uses the per-kernel launch path
+ * (tensor parallel, unsupported shapes, or YALM_ENGINE=0 at creation).
+ * yalm_time_kernel(d, 6, ...) times one greedy engine launch. */
+int yalm_decoder_engine(yalm_decoder d);
 
 /* ---------------- tensor parallelism (BASELINE config 5) ----------------
  * Megatron row/column split of one model over tp_size GPUs, one process per

@@ -9,6 +9,7 @@
 
 #include "../../include/yalm_hip.h"
 #include "device_common.h"
+#include "engine.h"
 
 // ------------------------------------------------------------------ errors
 void set_err(const std::string &s); // yalm_hip.hip (thread-local last error)
@@ -105,5 +106,25 @@ struct yalm_decoder_s {
 	float *ipc_own = nullptr;        // this rank's buffer
 	float **ipc_bufs = nullptr;      // device array [tp_size] of buffer bases (peers opened via IPC)
 	std::vector<void *> ipc_opened;  // hipIpcOpenMemHandle mappings to close
+	// persistent per-token engine (engine.h): one launch per token when the
+	// config is supported (single GPU, head_dim 128, G <= 4, dims multiple of
+	// 64 * EPL and <= 16384); YALM_ENGINE=0 selects the launch path
+	bool engine = false;
+	int eng_nb = 0;                  // workgroups = CUs
+	EngLayer *eng_layers = nullptr;  // [n_layers]
+	unsigned *eng_flags = nullptr;   // [round_up(NB, 256)] per-CU epochs
+	unsigned *eng_gen = nullptr;     // launch generation
+	unsigned *eng_err = nullptr;     // error bits (ENG_ERR_*)
+	unsigned *eng_tickets = nullptr; // [n_kv] attention arrival tickets
+	float *eng_part = nullptr;       // [n_heads][ENG_SMAX][head_dim + 2] split partials
+	float *eng_amax = nullptr;       // [NB][2] per-CU (max, index)
+	EngArgs *eng_args = nullptr;     // [N_GRAPHS] kernel arguments per mode (device)
 };
 
+// ------------------------------------------------------------------ shared helpers
+int dalloc(yalm_decoder_s *d, void **p, size_t bytes); // zeroed device allocation owned by d
+
+// persistent engine (engine.hip)
+int engine_init(yalm_decoder_s *d);                // enables d->engine when supported
+int engine_enqueue(yalm_decoder_s *d, int which);  // one launch = one token (graph `which`)
+int engine_check(yalm_decoder_s *d);               // after a sync: bounded spins that gave up

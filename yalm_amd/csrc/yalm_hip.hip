@@ -512,6 +512,13 @@ static int enqueue_begin_t(yalm_decoder_s *d) {
 	                       : FN<WF8>(__VA_ARGS__))
 
 static int enqueue_forward(yalm_decoder_s *d, int which) {
+	if (d->engine) {
+		TRY(engine_enqueue(d, which));
+		if (which == GRAPH_LOGITS)
+			HIPCHK(hipMemcpyAsync(d->logits_pinned, d->logits, sizeof(float) * d->vocab_full, hipMemcpyDeviceToHost,
+			                      d->stream));
+		return YALM_OK;
+	}
 	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_begin_t, d));
 	for (int l = 0; l < d->c.n_layers; ++l)
 		TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_layer_t, d, l));
@@ -617,7 +624,7 @@ static void destroy_decoder(yalm_decoder_s *d) {
 	delete d;
 }
 
-static int dalloc(yalm_decoder_s *d, void **p, size_t bytes) {
+int dalloc(yalm_decoder_s *d, void **p, size_t bytes) {
 	HIPCHK(hipMalloc(p, bytes ? bytes : 4));
 	d->dev_allocs.push_back(*p);
 	HIPCHK(hipMemset(*p, 0, bytes ? bytes : 4));
@@ -708,6 +715,8 @@ static int create_decoder(const yalm_config *config, const yalm_model_weights *w
 		set_err("hipHostMalloc failed");
 		return fail(YALM_ERR_HIP);
 	}
+	if ((r = engine_init(d)))
+		return fail(r);
 	if (hipDeviceSynchronize() != hipSuccess) {
 		set_err("hipDeviceSynchronize failed after decoder allocation");
 		return fail(YALM_ERR_HIP);
@@ -817,6 +826,7 @@ extern "C" int yalm_decoder_create_tp_ipc(const yalm_config *config, const yalm_
 	}
 	yalm_decoder_s *d = *out;
 	d->ipc = true;
+	d->engine = false; // the engine is single-GPU only
 	d->ipc_S = ipc_slot_floats(*config, tp_size);
 	d->ipc_own = (float *)own_buf;
 	d->ipc_opened = opened;
@@ -858,6 +868,7 @@ extern "C" int yalm_forward(yalm_decoder d, int token, int pos, int mode, float 
 	TRY(replay(d, which));
 	if (which == GRAPH_LOGITS) {
 		HIPCHK(hipStreamSynchronize(d->stream));
+		TRY(engine_check(d));
 		if (logits_host)
 			memcpy(logits_host, d->logits_pinned, sizeof(float) * d->vocab_full);
 	}
@@ -890,6 +901,7 @@ extern "C" int yalm_generate_greedy(yalm_decoder d, int token, int pos, int n_st
 			TRY(replay(d, GRAPH_GREEDY));
 		HIPCHK(hipMemcpyAsync(out_tokens + done, d->tokens, sizeof(int) * batch, hipMemcpyDeviceToHost, d->stream));
 		HIPCHK(hipStreamSynchronize(d->stream));
+		TRY(engine_check(d));
 		done += batch;
 	}
 	return YALM_OK;
@@ -899,6 +911,7 @@ extern "C" int yalm_device_step(yalm_decoder d, int *token, int *pos) {
 	ARGCHK(d, "null decoder");
 	StepState s;
 	HIPCHK(hipStreamSynchronize(d->stream));
+	TRY(engine_check(d));
 	HIPCHK(hipMemcpy(&s, d->step, sizeof(s), hipMemcpyDeviceToHost));
 	if (token)
 		*token = s.token;
@@ -995,11 +1008,31 @@ static int enqueue_one_t(yalm_decoder_s *d, int kernel_id, int l) {
 	return YALM_ERR_ARG;
 }
 
+extern "C" int yalm_decoder_engine(yalm_decoder d) {
+	return d && d->engine ? 1 : 0;
+}
+
 extern "C" int yalm_time_kernel(yalm_decoder d, int kernel_id, int iters, float *avg_ms) {
-	ARGCHK(d && avg_ms && iters > 0 && kernel_id >= 0 && kernel_id <= 5, "bad argument");
+	ARGCHK(d && avg_ms && iters > 0 && kernel_id >= 0 && kernel_id <= 6, "bad argument");
+	ARGCHK(kernel_id != 6 || d->engine, "kernel 6 (engine) needs a decoder running the persistent engine");
 	hipEvent_t e0, e1;
 	HIPCHK(hipEventCreate(&e0));
 	HIPCHK(hipEventCreate(&e1));
+	if (kernel_id == 6) { // back-to-back greedy engine launches (each one token)
+		TRY(engine_enqueue(d, GRAPH_GREEDY));
+		HIPCHK(hipEventRecord(e0, d->stream));
+		for (int i = 0; i < iters; ++i)
+			TRY(engine_enqueue(d, GRAPH_GREEDY));
+		HIPCHK(hipEventRecord(e1, d->stream));
+		HIPCHK(hipEventSynchronize(e1));
+		TRY(engine_check(d));
+		float ms = 0.f;
+		HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+		(void)hipEventDestroy(e0);
+		(void)hipEventDestroy(e1);
+		*avg_ms = ms / iters;
+		return YALM_OK;
+	}
 	// warm-up once, then time; rotate layers so weights come from HBM, not the
 	// 256 MiB Infinity Cache.
 	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_one_t, d, kernel_id, 0));
@@ -1043,6 +1076,9 @@ extern "C" const char *yalm_kernel_name(yalm_decoder d, int kernel_id) {
 	static const bool legacy = getenv("YALM_GEMV_LEGACY") && atoi(getenv("YALM_GEMV_LEGACY")) != 0;
 	const std::string gk = legacy ? "gemv_stream_kernel<" : "gemv_rb_kernel<";
 	switch (kernel_id) {
+	case 6:
+		s = std::string("engine_kernel<") + wt + ", ";
+		break;
 	case 0:
 		s = gk + wt + ", PQKV<";
 		break;

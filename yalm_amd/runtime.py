@@ -104,6 +104,7 @@ _sig("yalm_get_logits", c_int, [c_void_p, c_void_p])
 _sig("yalm_time_kernel", c_int, [c_void_p, c_int, c_int, ctypes.POINTER(c_float)])
 _sig("yalm_kernel_name", ctypes.c_char_p, [c_void_p, c_int])
 _sig("yalm_set_gemv_config", c_int, [c_void_p, c_int, c_int, c_int, c_int])
+_sig("yalm_decoder_engine", c_int, [c_void_p])
 _sig("yalm_matmul", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int])
 _sig("yalm_mha", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int])
 _sig("yalm_ffn", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int])
@@ -125,6 +126,7 @@ EXPORTED = [
     "yalm_time_kernel", "yalm_kernel_name", "yalm_set_gemv_config", "yalm_matmul", "yalm_mha", "yalm_ffn",
     "yalm_prefill", "yalm_prefill_time", "yalm_gemm_f16", "yalm_attn_prefill", "yalm_tp_unique_id",
     "yalm_decoder_create_tp", "yalm_copy_2d", "yalm_tp_ipc_alloc", "yalm_decoder_create_tp_ipc",
+    "yalm_decoder_engine",
 ]
 
 HYDRATE_KV_CACHE, OUTPUT_LOGITS = 0, 1
@@ -414,6 +416,11 @@ class Decoder:
 
     def set_gemv_config(self, kind: int, threads: int = 0, unroll: int = 0, gpw: int = 0) -> None:
         check(lib.yalm_set_gemv_config(self.h, kind, threads, unroll, gpw))
+
+    @property
+    def engine(self) -> bool:
+        """True when each token runs as one persistent engine launch (engine.h)."""
+        return bool(lib.yalm_decoder_engine(self.h))
 
     def kernel_name(self, kernel_id: int) -> str:
         return lib.yalm_kernel_name(self.h, kernel_id).decode()
