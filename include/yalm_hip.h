@@ -150,9 +150,18 @@ int yalm_set_gemv_config(yalm_decoder d, int kind, int threads, int unroll, int 
 const char *yalm_kernel_name(yalm_decoder d, int kernel_id);
 /* 1 if this decoder runs each token as ONE persistent launch (engine.h: LDS-DMA
  * weight ring + in-launch epoch seams), 0 if it uses the per-kernel launch path
- * (tensor parallel, unsupported shapes, or YALM_ENGINE=0 at creation).
+ * (tensor parallel, unsupported shapes, or YALM_ENGINE unset/0 at creation: the
+ * engine is opt-in, YALM_ENGINE=1).
  * yalm_time_kernel(d, 6, ...) times one greedy engine launch. */
 int yalm_decoder_engine(yalm_decoder d);
+/* Timeline of the engine's most recent launch (decoder created with
+ * YALM_ENGINE_TRACE=1): for workgroup w and phase p (5 per layer: QKV,
+ * attention, Wo, W1/W3, W2; then logits; the last index 5 L + 1 holds per-CU
+ * extras) 8 words at [(w * (5 L + 2) + p) * 8 + k]: s_memrealtime (100 MHz) at
+ * phase start / input ready / rows done / published, loader ring-full ticks so
+ * far, ring slots landed and consumer item position at phase start.
+ * Copies min(count, total) words; *workgroups = grid size. Profiling hook. */
+int yalm_engine_trace(yalm_decoder d, unsigned long long *host, size_t count, int *workgroups);
 
 /* ---------------- tensor parallelism (BASELINE config 5) ----------------
  * Megatron row/column split of one model over tp_size GPUs, one process per

@@ -119,6 +119,7 @@ struct yalm_decoder_s {
 	float *eng_part = nullptr;       // [n_heads][ENG_SMAX][head_dim + 2] split partials
 	float *eng_amax = nullptr;       // [NB][2] per-CU (max, index)
 	EngArgs *eng_args = nullptr;     // [N_GRAPHS] kernel arguments per mode (device)
+	unsigned long long *eng_trace = nullptr; // YALM_ENGINE_TRACE=1: [NB][5 L + 2][8] stamps
 };
 
 // ------------------------------------------------------------------ shared helpers

@@ -43,8 +43,8 @@
 #define ENG_LDS __attribute__((address_space(3)))
 #define ENG_ITEM 1024                        // one wave-wide 16 B/lane load
 #define ENG_IPS 8                            // items per ring slot (8 KB)
-#define ENG_INFLIGHT 7                       // slots in flight: ENG_IPS * ENG_INFLIGHT <= 63 (vmcnt)
-#define ENG_INFLIGHT_LOADS "56"              // = ENG_IPS * ENG_INFLIGHT, for the s_waitcnt string
+#define ENG_LD 2                             // own slots in flight per loader wave
+#define ENG_LD_LOADS "16"                    // = ENG_IPS * ENG_LD, for the s_waitcnt string
 #define ENG_MAXROWS 512                      // rows of one phase per CU (row partials in LDS)
 #define ENG_KC 32                            // attention keys per chunk (one wave, 8 rows per lane)
 #define ENG_SMAX 32                          // attention splits per kv head
@@ -57,8 +57,9 @@ enum { EM_HYDRATE = 0, EM_LOGITS = 1, EM_GREEDY = 2 };
 enum { ENG_ERR_SEAM = 1, ENG_ERR_RING = 2, ENG_ERR_CBAR = 4, ENG_ERR_ABORT = 8 };
 
 // control words in LDS
-enum { CTL_FULL = 0, CTL_CONS = 1 /* .. 1 + C */, CTL_CBAR = 9, CTL_SEAM = 10, CTL_ABORT = 11, CTL_NRM = 16,
-       CTL_AMAX = 32 };
+enum { CTL_FULL = 0 /* .. + L: own slots landed per loader */, CTL_CONS = 4 /* .. + C */, CTL_CBAR = 12,
+       CTL_SEAM = 13, CTL_ABORT = 14, CTL_NRM = 16, CTL_AMAX = 32,
+       CTL_LSTALL = 48 /* .. + L: ring-full ticks per loader; 52, 53: finish time lo/hi */ };
 
 struct EngLayer {
 	const char *wq, *wk, *wv, *wo, *w1, *w2, *w3;
@@ -78,6 +79,11 @@ struct EngArgs {
 	float *x, *q, *xb2, *hb, *logits, *part, *amax;
 	unsigned *tickets, *flags, *gen, *err;
 	int *tokens;
+	unsigned long long *trace; // [NB][5 L + 2][8] s_memrealtime stamps of the last launch (null: off)
+	int dbg;      // timing-only ablations (YALM_ENGINE_DBG): 1 = no FMA math, 2 = no seams, 4 = consumers skip the ring
+	int ld_depth; // own slots in flight per loader wave (1..7; YALM_ENGINE_DEPTH)
+	int ld_nt;    // weight stream cache policy: 1 = nt (default), 0 = default policy (YALM_ENGINE_NT)
+	int ld_waves; // loader waves that stream (1..NL; YALM_ENGINE_LOADERS); the others exit
 };
 
 template <int C>
@@ -129,12 +135,46 @@ __device__ __forceinline__ void eng_lds_rel(volatile ENG_LDS unsigned *p, unsign
 // 16-byte LDS-DMA of one lane's piece (MI355X_MICROARCH / cdna_hip_programming.md §5.7
 // recipe): M0 = wave-uniform LDS destination; lane i lands at M0 + 16 i. Hidden from
 // hipcc's waitcnt bookkeeping on purpose: the loader counts its own vmcnt.
-__device__ __forceinline__ void eng_glds16(const void *g, unsigned lds_dst) {
+__device__ __forceinline__ void eng_glds16(const void *g, unsigned lds_dst, bool nt) {
 	unsigned keep;
-	asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-	             : "=&s"(keep)
-	             : "v"(g), "s"(lds_dst)
-	             : "memory");
+	if (nt)
+		asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+		             : "=&s"(keep)
+		             : "v"(g), "s"(lds_dst)
+		             : "memory");
+	else
+		asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+		             : "=&s"(keep)
+		             : "v"(g), "s"(lds_dst)
+		             : "memory");
+}
+// wait until at most d own slots (8 loads each) of this wave are still in flight
+__device__ __forceinline__ void eng_vmcnt_slots(int d) {
+	switch (d) {
+	case 0:
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		break;
+	case 1:
+		asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+		break;
+	case 2:
+		asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+		break;
+	case 3:
+		asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+		break;
+	case 4:
+		asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+		break;
+	case 5:
+		asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
+		break;
+	case 6:
+		asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+		break;
+	default:
+		asm volatile("s_waitcnt vmcnt(56)" ::: "memory");
+	}
 }
 
 // one element of a weight row (embedding residual of layer 0)
@@ -161,6 +201,57 @@ __device__ __forceinline__ void fma_chunk_eng(float &acc, const u32x4_t &w, cons
 		a1 = fmaf(wf[e + 1], x[e + 1], a1);
 	}
 	acc += a0 + a1;
+}
+
+// f16 weight (lo / hi half of a dword) x f32 activation + f32 accumulator in ONE
+// instruction: v_fma_mix_f32 widens the f16 operand exactly and rounds once, so it
+// equals cvt + fma bit for bit at half the instruction count.
+__device__ __forceinline__ float eng_fma_mix_lo(uint32_t w2, float x, float acc) {
+	float d;
+	asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(d) : "v"(w2), "v"(x), "v"(acc));
+	return d;
+}
+__device__ __forceinline__ float eng_fma_mix_hi(uint32_t w2, float x, float acc) {
+	float d;
+	asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(d) : "v"(w2), "v"(x), "v"(acc));
+	return d;
+}
+// acc += w . x over one 16-byte piece, two independent chains
+template <class WT>
+__device__ __forceinline__ void eng_dot16(float &a0, float &a1, const u32x4_t &w, const float (&x)[WT::EPL]) {
+	if constexpr (WT::BYTES == 2) {
+		// one statement: no compiler pads between the dependent (hardware-interlocked) VALU ops
+		asm("v_fma_mix_f32 %0, %2, %4, %0 op_sel_hi:[1,0,0]\n\t"
+		    "v_fma_mix_f32 %1, %2, %5, %1 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+		    "v_fma_mix_f32 %0, %3, %6, %0 op_sel_hi:[1,0,0]\n\t"
+		    "v_fma_mix_f32 %1, %3, %7, %1 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+		    : "+v"(a0), "+v"(a1)
+		    : "v"(w[0]), "v"(w[1]), "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]));
+		asm("v_fma_mix_f32 %0, %2, %4, %0 op_sel_hi:[1,0,0]\n\t"
+		    "v_fma_mix_f32 %1, %2, %5, %1 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+		    "v_fma_mix_f32 %0, %3, %6, %0 op_sel_hi:[1,0,0]\n\t"
+		    "v_fma_mix_f32 %1, %3, %7, %1 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+		    : "+v"(a0), "+v"(a1)
+		    : "v"(w[2]), "v"(w[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]));
+	} else {
+		float wf[WT::EPL];
+		WT::unpack(w, wf);
+#pragma unroll
+		for (int e = 0; e < WT::EPL; e += 2) {
+			a0 = fmaf(wf[e], x[e], a0);
+			a1 = fmaf(wf[e + 1], x[e + 1], a1);
+		}
+	}
+}
+// Sums of 4 per-lane values over the wave, transposed: lanes 16 t .. 16 t + 15 end
+// with the total of v[t]. Each exchange sends the value the partner keeps and keeps
+// the one it sends back (2 xor-32 + 1 xor-16 lane swaps), then one 16-lane DPP sum.
+__device__ __forceinline__ float eng_sum4_t(const float (&v)[4]) {
+	const bool hi32 = threadIdx.x & 32, odd16 = threadIdx.x & 16;
+	const float s02 = (hi32 ? v[2] : v[0]) + xor32(hi32 ? v[0] : v[2]); // lanes 0-31: row 0, 32-63: row 2
+	const float s13 = (hi32 ? v[3] : v[1]) + xor32(hi32 ? v[1] : v[3]); // row 1 / row 3
+	const float u = (odd16 ? s13 : s02) + xor16(odd16 ? s02 : s13);     // 16-lane group g: row g
+	return row16_sum(u);
 }
 
 // ---------------------------------------------------------------- phase geometry
@@ -237,53 +328,74 @@ __device__ __forceinline__ void eng_fail(unsigned *err, volatile ENG_LDS unsigne
 		__hip_atomic_fetch_or(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// ---------------------------------------------------------------- loader wave
-template <class WT, int C>
-__device__ __forceinline__ void eng_loader(const EngArgs &a, unsigned ring_lds, volatile ENG_LDS unsigned *ctl) {
+// ---------------------------------------------------------------- loader waves
+// L loader waves share the CU's item stream slot-interleaved: loader l issues the
+// 8 items of every slot s with s % L == l (one wave's DMA issue rate, ~8 GB/s,
+// is far below the CU's 25 GB/s share of HBM) and publishes how many of ITS
+// slots have landed (ctl[CTL_FULL + l]) behind its own counted vmcnt.
+template <class WT, int C, int NL>
+__device__ __forceinline__ void eng_loader(const EngArgs &a, unsigned ring_lds, volatile ENG_LDS unsigned *ctl, int l) {
 	constexpr int NS = eng_ring_slots<C>();
 	const int b = blockIdx.x, NB = gridDim.x, lane = threadIdx.x & 63;
 	const int nph = 5 * a.n_layers + (a.mode != EM_HYDRATE ? 1 : 0);
 	__builtin_amdgcn_s_setprio(3);
-	unsigned slot = 0, free_seen = NS; // slots < free_seen may be issued
-	int k = 0;
-	for (int ph = 0; ph < nph; ++ph) {
+	unsigned slot = 0, mine = 0, free_seen = NS, stall = 0;
+	const int depth = a.ld_depth;
+	const int nl = a.ld_waves;
+	if (l >= nl)
+		return;
+	const bool nt = a.ld_nt != 0;
+	int k = 0; // items of the current slot already walked
+	bool dead = false;
+	for (int ph = 0; ph < nph && !dead; ++ph) {
 		const int kind = eng_kind(a, ph);
 		if (kind == EK_ATTN)
 			continue;
-		const EngLayer &L = a.layers[ph < 5 * a.n_layers ? ph / 5 : 0];
+		const EngLayer &Ly = a.layers[ph < 5 * a.n_layers ? ph / 5 : 0];
 		int n, ngroups, R;
 		eng_geo(a, kind, n, ngroups, R);
 		const int nch = n * WT::BYTES / ENG_ITEM;
 		const int ngl = eng_ngl(ngroups, b, NB);
-		for (int gl = 0; gl < ngl; ++gl) {
-			for (int r = 0; r < R; ++r) {
-				const char *rp = eng_row<WT>(a, L, kind, b + gl * NB, r, n) + lane * 16;
-				for (int c = 0; c < nch; ++c) {
-					if (k == 0 && slot >= free_seen) { // wait until every consumer released slot - NS
-						EngSpin sp;
-						for (;;) {
-							unsigned m = ctl[CTL_CONS];
+		for (int gl = 0; gl < ngl && !dead; ++gl) {
+			for (int r = 0; r < R && !dead; ++r) {
+				const char *rp = eng_row<WT>(a, Ly, kind, b + gl * NB, r, n) + lane * 16;
+				for (int c = 0; c < nch;) {
+					const int take = min(nch - c, ENG_IPS - k); // this row's items in the current slot
+					if ((int)(slot % nl) == l) {
+						if (k == 0 && slot >= free_seen) { // ring position of slot - NS still in use
+							const unsigned long long ts = __builtin_amdgcn_s_memrealtime();
+							EngSpin sp;
+							for (;;) {
+								unsigned m = ctl[CTL_CONS];
 #pragma unroll
-							for (int w = 1; w < C; ++w)
-								m = min(m, (unsigned)ctl[CTL_CONS + w]);
-							free_seen = m + NS;
-							if (slot < free_seen)
-								break;
-							if (eng_spin(sp, ctl)) {
-								eng_fail(a.err, ctl, ENG_ERR_RING);
-								asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-								return;
+								for (int w = 1; w < C; ++w)
+									m = min(m, (unsigned)ctl[CTL_CONS + w]);
+								free_seen = m + NS;
+								if (slot < free_seen)
+									break;
+								if (eng_spin(sp, ctl)) {
+									eng_fail(a.err, ctl, ENG_ERR_RING);
+									dead = true;
+									break;
+								}
 							}
+							stall += (unsigned)(__builtin_amdgcn_s_memrealtime() - ts);
+							ctl[CTL_LSTALL + l] = stall;
+							if (dead)
+								break;
 						}
+						const unsigned dst = ring_lds + ((slot % NS) * ENG_IPS + k) * ENG_ITEM;
+						for (int i = 0; i < take; ++i)
+							eng_glds16(rp + (size_t)(c + i) * ENG_ITEM, __builtin_amdgcn_readfirstlane(dst + i * ENG_ITEM), nt);
 					}
-					eng_glds16(rp + (size_t)c * ENG_ITEM,
-					           __builtin_amdgcn_readfirstlane(ring_lds + ((slot % NS) * ENG_IPS + k) * ENG_ITEM));
-					if (++k == ENG_IPS) {
-						k = 0;
-						if (slot >= ENG_INFLIGHT) {
-							asm volatile("s_waitcnt vmcnt(" ENG_INFLIGHT_LOADS ")" ::: "memory");
-							ctl[CTL_FULL] = slot - ENG_INFLIGHT + 1;
+					c += take;
+					k += take;
+					if (k == ENG_IPS) {
+						if ((int)(slot % nl) == l && ++mine > (unsigned)depth) {
+							eng_vmcnt_slots(depth);
+							ctl[CTL_FULL + l] = mine - depth;
 						}
+						k = 0;
 						++slot;
 					}
 				}
@@ -291,11 +403,16 @@ __device__ __forceinline__ void eng_loader(const EngArgs &a, unsigned ring_lds, 
 		}
 	}
 	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-	ctl[CTL_FULL] = slot + (k ? 1 : 0);
+	if (k > 0 && (int)(slot % nl) == l)
+		++mine; // the partial last slot
+	ctl[CTL_FULL + l] = mine;
+	const unsigned long long tf = __builtin_amdgcn_s_memrealtime();
+	ctl[52] = (unsigned)tf;
+	ctl[53] = (unsigned)(tf >> 32);
 }
 
 // ---------------------------------------------------------------- consumer context
-template <class WT, int C>
+template <class WT, int C, int NL>
 struct EngCtx {
 	const EngArgs &a;
 	ENG_LDS char *ring;
@@ -326,28 +443,45 @@ struct EngCtx {
 		}
 	}
 
+	// slots landed as a contiguous prefix: loader l's first missing slot is count_l * NL + l
+	// (the NL <= 4 counters are one 16-byte LDS read)
+	__device__ __forceinline__ unsigned landed() {
+		static_assert(NL >= 1 && NL <= 4 && CTL_FULL % 4 == 0, "loader counters: one ds_read_b128");
+		const u32x4_t f = *(volatile ENG_LDS u32x4_t *)(ctl + CTL_FULL);
+		const unsigned nl = (unsigned)a.ld_waves;
+		unsigned m = f[0] * nl;
+#pragma unroll
+		for (int l = 1; l < NL; ++l) {
+			const unsigned v = f[l];
+			if (l < (int)nl)
+				m = min(m, v * nl + l);
+		}
+		return m;
+	}
 	// ring slot holding item j has landed
 	__device__ __forceinline__ bool wait_item(unsigned j) {
 		const unsigned s = j / ENG_IPS;
-		if (s < full_seen)
+		if (s < full_seen) {
+			asm volatile("" ::: "memory"); // no ring read may be hoisted above this check
 			return true;
+		}
 		EngSpin sp;
-		while ((full_seen = eng_lds_acq(&ctl[CTL_FULL])) <= s) {
+		while ((full_seen = landed()) <= s) {
 			if (eng_spin(sp, ctl)) {
 				eng_fail(a.err, ctl, ENG_ERR_RING);
 				dead = true;
 				return false;
 			}
 		}
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup"); // ring reads stay behind the poll
 		return true;
 	}
 	__device__ __forceinline__ u32x4_t ring_item(unsigned j) const {
 		constexpr unsigned RING = eng_ring_slots<C>() * ENG_IPS;
 		return *(const ENG_LDS u32x4_t *)(ring + (size_t)(j % RING) * ENG_ITEM + lane * 16);
 	}
-	__device__ __forceinline__ void release(unsigned next_item) {
-		if (lane == 0)
-			eng_lds_rel(&ctl[CTL_CONS + w], next_item / ENG_IPS);
+	__device__ __forceinline__ void release(unsigned next_item) { // every lane stores the same word
+		eng_lds_rel(&ctl[CTL_CONS + w], next_item / ENG_IPS);
 	}
 
 	// every CU finished phase `epoch` (flags are per-CU epochs, monotonic over launches)
@@ -398,9 +532,60 @@ struct EngCtx {
 	}
 };
 
+// The wave's share of a phase: for every row, its KW chunk columns (w, w + C, ...)
+// dotted with the register slice xr. Rows go in tiles of 4: one transposed
+// cross-lane reduction, one branch-free LDS write of the 4 row partials
+// (part[row][wave]; rows past the phase land in spare rows nobody reads) and one
+// ring release per tile.
+template <class WT, int C, int NL, int KW, bool MATH>
+__device__ __forceinline__ bool eng_rows(EngCtx<WT, C, NL> &cx, const float (&xr)[64 / WT::EPL][WT::EPL], int rows,
+                                         int nch) {
+	constexpr unsigned RING = eng_ring_slots<C>() * ENG_IPS;
+	const int w = cx.w, lane = cx.lane;
+	const unsigned lane_off = (unsigned)lane * 16;
+	for (int r0 = 0; r0 < rows; r0 += 4) {
+		float acc[4];
+#pragma unroll
+		for (int t = 0; t < 4; ++t) {
+			float a0 = 0.0f, a1 = 0.0f;
+			if (r0 + t < rows) {
+				const unsigned j0 = cx.jbase + (unsigned)(r0 + t) * nch + w;
+				// slots land in order: waiting for my last item of the row covers the others
+				if (!cx.wait_item(j0 + (KW - 1) * C))
+					return false;
+				unsigned pos = j0 % RING;
+				u32x4_t wv[KW];
+#pragma unroll
+				for (int k = 0; k < KW; ++k) {
+					wv[k] = *(const ENG_LDS u32x4_t *)(cx.ring + pos * ENG_ITEM + lane_off);
+					pos += C;
+					if (pos >= RING)
+						pos -= RING;
+				}
+				if constexpr (MATH) {
+#pragma unroll
+					for (int k = 0; k < KW; ++k)
+						eng_dot16<WT>(a0, a1, wv[k], xr[k]);
+				} else {
+#pragma unroll
+					for (int k = 0; k < KW; ++k)
+						a0 += __uint_as_float(wv[k][0] & 0x3fffffu);
+				}
+				// per row, not per tile: a tile of long rows (W2: 3.5 slots each) held until its
+				// end would pin more slots than the ring minus the loaders' publication lag
+				cx.release(j0 - w + nch);
+			}
+			acc[t] = a0 + a1;
+		}
+		const float tot = eng_sum4_t(acc);
+		cx.part[(r0 + (lane >> 4)) * C + w] = tot;
+	}
+	return true;
+}
+
 // ---------------------------------------------------------------- GEMV phase (consumers)
-template <class WT, int C>
-__device__ __forceinline__ void eng_gemv(EngCtx<WT, C> &cx, int kind, int layer) {
+template <class WT, int C, int NL>
+__device__ __forceinline__ void eng_gemv(EngCtx<WT, C, NL> &cx, int kind, int layer, unsigned long long *tr) {
 	constexpr int EPL = WT::EPL;
 	constexpr int KMAX = 64 / EPL; // x slice registers: KMAX x EPL = 64 floats per lane
 	constexpr int CH = 64 * EPL;   // elements per item
@@ -482,32 +667,51 @@ __device__ __forceinline__ void eng_gemv(EngCtx<WT, C> &cx, int kind, int layer)
 		}
 	}
 
-	// ---- stream the ring: row by row, my chunks of each row
+	if (tr)
+		tr[1] = __builtin_amdgcn_s_memrealtime();
+	// ---- stream the ring: row by row, my chunks of each row (count known at compile time)
+	const bool math = !(a.dbg & 1);
 	const int ngl = eng_ngl(ngroups, cx.b, cx.NB);
 	const int rows = ngl * R;
-	for (int rl = 0; rl < rows; ++rl) {
-		const unsigned j0 = cx.jbase + (unsigned)rl * nch;
-		// slots land in order: waiting for my last item of the row covers the others,
-		// then all of the row's LDS reads are in flight together
-		if (kw > 0 && !cx.wait_item(j0 + w + (kw - 1) * C))
-			return;
-		u32x4_t wv[KMAX];
-#pragma unroll
-		for (int k = 0; k < KMAX; ++k)
-			if (k < kw)
-				wv[k] = cx.ring_item(j0 + w + k * C);
-		float acc = 0.0f;
-#pragma unroll
-		for (int k = 0; k < KMAX; ++k)
-			if (k < kw)
-				fma_chunk_eng<WT>(acc, wv[k], xr[k]);
-		cx.release(j0 + nch);
-		const float s = wave_sum(acc);
-		if (lane == 0)
-			cx.part[rl * C + w] = s;
+	bool ok = true;
+	switch ((a.dbg & 4) ? 0 : kw) {
+#define ENG_ROWS_CASE(K)                                                                                               \
+	case K:                                                                                                            \
+		if constexpr (K <= KMAX)                                                                                       \
+			ok = math ? eng_rows<WT, C, NL, K, true>(cx, xr, rows, nch) : eng_rows<WT, C, NL, K, false>(cx, xr, rows, nch); \
+		break;
+		ENG_ROWS_CASE(1)
+		ENG_ROWS_CASE(2)
+		ENG_ROWS_CASE(3)
+		ENG_ROWS_CASE(4)
+		ENG_ROWS_CASE(5)
+		ENG_ROWS_CASE(6)
+		ENG_ROWS_CASE(7)
+		ENG_ROWS_CASE(8)
+		ENG_ROWS_CASE(9)
+		ENG_ROWS_CASE(10)
+		ENG_ROWS_CASE(11)
+		ENG_ROWS_CASE(12)
+		ENG_ROWS_CASE(13)
+		ENG_ROWS_CASE(14)
+		ENG_ROWS_CASE(15)
+		ENG_ROWS_CASE(16)
+#undef ENG_ROWS_CASE
+	default: // no chunk of this phase's rows: zero partials, keep releasing
+		for (int rl = 0; rl < rows; ++rl) {
+			if (!(a.dbg & 4))
+				cx.release(cx.jbase + (unsigned)(rl + 1) * nch);
+			if (lane == 0)
+				cx.part[rl * C + w] = 0.0f;
+		}
 	}
+	if (!ok)
+		return;
 	cx.jbase += (unsigned)rows * nch;
-	cx.release(cx.jbase);
+	if (!(a.dbg & 4))
+		cx.release(cx.jbase);
+	if (tr)
+		tr[2] = __builtin_amdgcn_s_memrealtime();
 	cx.cbar(); // row partials of every wave are in LDS
 
 	// ---- epilogue: one thread per row group, partials summed in wave order
@@ -773,8 +977,8 @@ __device__ __forceinline__ void eng_attn_unit(const EngArgs &a, const EngLayer &
 }
 
 // ---------------------------------------------------------------- the kernel
-template <class WT, int C, int GT>
-__global__ __launch_bounds__(64 * (C + 1)) void engine_kernel(const EngArgs *__restrict__ args) {
+template <class WT, int C, int NL, int GT>
+__global__ __launch_bounds__(64 * (C + NL)) void engine_kernel(const EngArgs *__restrict__ args) {
 	// Arguments live in device memory (written once per decoder and mode): a
 	// by-value struct whose address is taken is copied to scratch per lane.
 	const EngArgs &a = *args;
@@ -789,12 +993,12 @@ __global__ __launch_bounds__(64 * (C + 1)) void engine_kernel(const EngArgs *__r
 	__syncthreads(); // the only workgroup barrier: loader and consumers split after it
 
 	const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-	if (wave == C) {
-		eng_loader<WT, C>(a, (unsigned)(uintptr_t)ring, ctl);
+	if (wave >= C) {
+		eng_loader<WT, C, NL>(a, (unsigned)(uintptr_t)ring, ctl, wave - C);
 		return;
 	}
 
-	EngCtx<WT, C> cx(a);
+	EngCtx<WT, C, NL> cx(a);
 	cx.ring = ring;
 	cx.part = part;
 	cx.ctl = ctl;
@@ -816,14 +1020,25 @@ __global__ __launch_bounds__(64 * (C + 1)) void engine_kernel(const EngArgs *__r
 	cx.kv_pos = cx.kv_sink + (cx.pos - cx.kv_sink) % (a.max_seq_len - cx.kv_sink);
 	cx.kv_len = cx.pos >= a.max_seq_len ? a.max_seq_len : cx.pos + 1;
 
+	if ((a.dbg & 4) && cx.lane == 0) // timing only: the loaders stream unthrottled
+		ctl[CTL_CONS + cx.w] = 0x40000000u;
 	const int nph = 5 * a.n_layers + (a.mode != EM_HYDRATE ? 1 : 0);
+	unsigned long long *trb = a.trace && cx.w == 0 && cx.lane == 0 ? a.trace + (size_t)cx.b * E * 8 : nullptr;
+	if (trb)
+		trb[(E - 1) * 8] = __builtin_amdgcn_s_memrealtime();
 	for (int ph = 0; ph < nph && !cx.dead; ++ph) {
 		const int kind = eng_kind(a, ph);
 		const int layer = ph < 5 * a.n_layers ? ph / 5 : 0;
-		if (ph > 0)
+		if (ph > 0 && !(a.dbg & 2))
 			cx.seam(cx.epoch0 + ph); // phase ph - 1 done everywhere
 		if (cx.dead)
 			break;
+		unsigned long long *tr = trb ? trb + (size_t)ph * 8 : nullptr;
+		if (tr) {
+			tr[0] = __builtin_amdgcn_s_memrealtime();
+			tr[5] = cx.landed();
+			tr[6] = cx.jbase;
+		}
 		if (kind == EK_ATTN) {
 			const int G = a.n_heads / a.n_kv;
 			const int ns = (cx.kv_len + ENG_KC - 1) / ENG_KC;
@@ -831,10 +1046,21 @@ __global__ __launch_bounds__(64 * (C + 1)) void engine_kernel(const EngArgs *__r
 			const EngLayer &L = a.layers[layer];
 			for (int u = cx.b + cx.w * cx.NB; u < a.n_kv * S; u += cx.NB * C)
 				eng_attn_unit<GT>(a, L, u / S, u % S, S, ns, cx.kv_len, G, cx.lane, cx.dead, ctl, layer);
+			if (tr)
+				tr[1] = tr[2] = __builtin_amdgcn_s_memrealtime();
 		} else {
-			eng_gemv<WT, C>(cx, kind, layer);
+			eng_gemv<WT, C>(cx, kind, layer, tr);
 		}
 		cx.publish(cx.epoch0 + ph + 1);
+		if (tr) {
+			tr[3] = __builtin_amdgcn_s_memrealtime();
+			tr[4] = ctl[CTL_LSTALL];
+		}
+	}
+	if (trb) { // per-CU extras in the last record: start, loader stall, loader finish, end
+		trb[(E - 1) * 8 + 1] = ctl[CTL_LSTALL];
+		trb[(E - 1) * 8 + 2] = (unsigned long long)ctl[52] | ((unsigned long long)ctl[53] << 32);
+		trb[(E - 1) * 8 + 3] = __builtin_amdgcn_s_memrealtime();
 	}
 	if (cx.dead)
 		return;

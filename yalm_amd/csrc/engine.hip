@@ -3,20 +3,22 @@
 // decoder's per-mode hipGraph like the launch path), error reporting.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
 #include "decoder.h"
 
-#define ENG_C 4 // consumer waves per CU (+1 loader wave)
+#define ENG_C 4 // consumer waves per CU
+#define ENG_L 4 // loader waves per CU
 
 template <class WT>
 static const void *engine_fn(int G) {
 	if (G <= 1)
-		return (const void *)engine_kernel<WT, ENG_C, 1>;
+		return (const void *)engine_kernel<WT, ENG_C, ENG_L, 1>;
 	if (G <= 2)
-		return (const void *)engine_kernel<WT, ENG_C, 2>;
-	return (const void *)engine_kernel<WT, ENG_C, 4>;
+		return (const void *)engine_kernel<WT, ENG_C, ENG_L, 2>;
+	return (const void *)engine_kernel<WT, ENG_C, ENG_L, 4>;
 }
 
 static const void *engine_fn_dt(int dtype, int G) {
@@ -45,14 +47,15 @@ static bool engine_supported(const yalm_decoder_s *d, int nb, std::string *why) 
 		if (n % CH != 0 || n > (64 / epl) * ENG_C * CH)
 			return no("GEMV input length not a multiple of 64 * EPL, or longer than the register slice");
 	auto rows = [&](int groups, int R) { return (groups + nb - 1) / nb * R; };
-	if (rows((q_dim + 2 * kv_dim) / 2, 2) > ENG_MAXROWS || rows(c.hidden_dim, 2) > ENG_MAXROWS ||
-	    rows(c.dim, 1) > ENG_MAXROWS || rows(c.vocab_size, 1) > ENG_MAXROWS)
+	constexpr int maxrows = ENG_MAXROWS - 4; // 4-row tiles may write up to 3 spare rows
+	if (rows((q_dim + 2 * kv_dim) / 2, 2) > maxrows || rows(c.hidden_dim, 2) > maxrows || rows(c.dim, 1) > maxrows ||
+	    rows(c.vocab_size, 1) > maxrows)
 		return no("too many rows per CU");
 	int occ = 0;
 	const void *fn = engine_fn_dt(c.weight_dtype, G);
 	if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)eng_lds_bytes<ENG_C>()) !=
 	        hipSuccess ||
-	    hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 64 * (ENG_C + 1), eng_lds_bytes<ENG_C>()) !=
+	    hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 64 * (ENG_C + ENG_L), eng_lds_bytes<ENG_C>()) !=
 	        hipSuccess ||
 	    occ < 1)
 		return no("engine kernel does not fit one workgroup per CU");
@@ -60,8 +63,9 @@ static bool engine_supported(const yalm_decoder_s *d, int nb, std::string *why) 
 }
 
 int engine_init(yalm_decoder_s *d) {
+	// opt-in until it beats the launch path on the bench workload
 	const char *env = getenv("YALM_ENGINE");
-	if (env && atoi(env) == 0)
+	if (!env || atoi(env) == 0)
 		return YALM_OK;
 	const int nb = device_cu_count();
 	if (!engine_supported(d, nb, nullptr))
@@ -84,6 +88,17 @@ int engine_init(yalm_decoder_s *d) {
 	TRY(dalloc(d, (void **)&d->eng_amax, sizeof(float) * 2 * nb));
 	TRY(dalloc(d, (void **)&d->eng_args, sizeof(EngArgs) * N_GRAPHS));
 	HIPCHK(hipMemcpy(d->eng_layers, L.data(), sizeof(EngLayer) * c.n_layers, hipMemcpyHostToDevice));
+	const char *tenv = getenv("YALM_ENGINE_TRACE");
+	if (tenv && atoi(tenv) != 0)
+		TRY(dalloc(d, (void **)&d->eng_trace, sizeof(unsigned long long) * nb * (5 * c.n_layers + 2) * 8));
+	const char *denv = getenv("YALM_ENGINE_DBG");
+	const int dbg = denv ? atoi(denv) : 0;
+	const char *depth_env = getenv("YALM_ENGINE_DEPTH");
+	const int depth = depth_env ? std::max(1, std::min(7, atoi(depth_env))) : ENG_LD;
+	const char *nt_env = getenv("YALM_ENGINE_NT");
+	const int ld_nt = nt_env ? atoi(nt_env) != 0 : 1;
+	const char *lw_env = getenv("YALM_ENGINE_LOADERS");
+	const int ld_waves = lw_env ? std::max(1, std::min(ENG_L, atoi(lw_env))) : ENG_L;
 
 	EngArgs a[N_GRAPHS];
 	for (int which = 0; which < N_GRAPHS; ++which) {
@@ -120,6 +135,11 @@ int engine_init(yalm_decoder_s *d) {
 		e.gen = d->eng_gen;
 		e.err = d->eng_err;
 		e.tokens = d->tokens;
+		e.trace = d->eng_trace;
+		e.dbg = dbg;
+		e.ld_depth = depth;
+		e.ld_nt = ld_nt;
+		e.ld_waves = ld_waves;
 	}
 	HIPCHK(hipMemcpy(d->eng_args, a, sizeof(a), hipMemcpyHostToDevice));
 	d->eng_nb = nb;
@@ -131,14 +151,14 @@ template <class WT>
 static int launch_engine_t(yalm_decoder_s *d, int which) {
 	const int G = d->c.n_heads / d->c.n_kv_heads;
 	const size_t lds = eng_lds_bytes<ENG_C>();
-	const dim3 grid(d->eng_nb), block(64 * (ENG_C + 1));
+	const dim3 grid(d->eng_nb), block(64 * (ENG_C + ENG_L));
 	const EngArgs *a = d->eng_args + which;
 	if (G <= 1)
-		hipLaunchKernelGGL((engine_kernel<WT, ENG_C, 1>), grid, block, lds, d->stream, a);
+		hipLaunchKernelGGL((engine_kernel<WT, ENG_C, ENG_L, 1>), grid, block, lds, d->stream, a);
 	else if (G <= 2)
-		hipLaunchKernelGGL((engine_kernel<WT, ENG_C, 2>), grid, block, lds, d->stream, a);
+		hipLaunchKernelGGL((engine_kernel<WT, ENG_C, ENG_L, 2>), grid, block, lds, d->stream, a);
 	else
-		hipLaunchKernelGGL((engine_kernel<WT, ENG_C, 4>), grid, block, lds, d->stream, a);
+		hipLaunchKernelGGL((engine_kernel<WT, ENG_C, ENG_L, 4>), grid, block, lds, d->stream, a);
 	HIPCHK(hipGetLastError());
 	return YALM_OK;
 }
@@ -165,5 +185,16 @@ int engine_check(yalm_decoder_s *d) {
 		        "): grid not co-resident or a CU stalled; YALM_ENGINE=0 selects the launch path");
 		return YALM_ERR_HIP;
 	}
+	return YALM_OK;
+}
+
+extern "C" int yalm_engine_trace(yalm_decoder d, unsigned long long *host, size_t count, int *workgroups) {
+	ARGCHK(d && host, "null argument");
+	ARGCHK(d->engine && d->eng_trace, "no engine trace (create the decoder with YALM_ENGINE_TRACE=1)");
+	HIPCHK(hipStreamSynchronize(d->stream));
+	const size_t total = (size_t)d->eng_nb * (5 * d->c.n_layers + 2) * 8;
+	HIPCHK(hipMemcpy(host, d->eng_trace, sizeof(unsigned long long) * std::min(count, total), hipMemcpyDeviceToHost));
+	if (workgroups)
+		*workgroups = d->eng_nb;
 	return YALM_OK;
 }
