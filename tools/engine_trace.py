@@ -35,7 +35,8 @@ def summarise(tr, L, label=""):
     end = tr[:, E - 1, 3]
     print(f"{label}kernel span {(end.max() - t0) / 100:.1f} us; CU start spread {(start.max() - t0) / 100:.2f} us; "
           f"loader stall total median {np.median(tr[:, E - 1, 1]) / 100:.1f} us, loader finish "
-          f"{(np.median(tr[:, E - 1, 2]) - t0) / 100:.1f} us")
+          f"{(np.median(tr[:, E - 1, 2]) - t0) / 100:.1f} us; loader0 vmcnt-wait median "
+          f"{np.median(tr[:, E - 1, 4]) / 100:.1f} us of lifetime {np.median(tr[:, E - 1, 5]) / 100:.1f} us")
     print(f"{'phase':8s} {'seam':>7s} {'in':>7s} {'rows':>7s} {'epi':>7s} {'crit':>7s} {'stall':>7s} {'ahead':>6s}")
     tot = 0.0
     for k, name in enumerate(KINDS + ["logits"]):

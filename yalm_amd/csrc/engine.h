@@ -41,6 +41,7 @@
 #include "device_common.h"
 
 #define ENG_LDS __attribute__((address_space(3)))
+#define ENG_CONST __attribute__((address_space(4))) // read-only for the launch: s_load (lgkmcnt only)
 #define ENG_ITEM 1024                        // one wave-wide 16 B/lane load
 #define ENG_IPS 8                            // items per ring slot (8 KB)
 #define ENG_LD 2                             // own slots in flight per loader wave
@@ -51,6 +52,8 @@
 #define ENG_D 128                            // head_dim supported by the engine
 #define ENG_TIMEOUT 200000000ull             // 2 s of s_memrealtime (100 MHz)
 #define ENG_CTL_WORDS 64
+#define ENG_PF_PAD 256                       // LDS landing pad of the prefetch wave's 4-B touches
+#define ENG_PF_LINE 64                       // prefetch touch stride (bytes per lane)
 
 enum { EK_QKV = 0, EK_ATTN = 1, EK_WO = 2, EK_GLU = 3, EK_W2 = 4, EK_LOGITS = 5 };
 enum { EM_HYDRATE = 0, EM_LOGITS = 1, EM_GREEDY = 2 };
@@ -80,19 +83,35 @@ struct EngArgs {
 	unsigned *tickets, *flags, *gen, *err;
 	int *tokens;
 	unsigned long long *trace; // [NB][5 L + 2][8] s_memrealtime stamps of the last launch (null: off)
-	int dbg;      // timing-only ablations (YALM_ENGINE_DBG): 1 = no FMA math, 2 = no seams, 4 = consumers skip the ring
+	int dbg;      // timing-only ablations (YALM_ENGINE_DBG): 1 = no FMA math, 2 = no seams, 4 = consumers skip the ring,
+	              // 32 = no epilogue / publish stores, 64 = no input gather
 	int ld_depth; // own slots in flight per loader wave (1..7; YALM_ENGINE_DEPTH)
 	int ld_nt;    // weight stream cache policy: 1 = nt (default), 0 = default policy (YALM_ENGINE_NT)
 	int ld_waves; // loader waves that stream (1..NL; YALM_ENGINE_LOADERS); the others exit
+	int poll_sleep; // consumers' s_sleep between ring polls (1, 2, 4, 8, 16; YALM_ENGINE_SLEEP)
+	int pf_ahead;   // items the prefetch wave (loader wave index ld_waves) runs ahead of the landed ring;
+	                // 0 = no prefetch wave (YALM_ENGINE_PF, in KB)
 };
+// EngArgs and the EngLayer table are read-only for a launch: every read goes through
+// these constant-address-space views, so it is an s_load (lgkmcnt). Read through a
+// generic pointer it would be a vector load re-issued after every memory-clobbering
+// asm (the ring polls and DMAs) and guarded by a vmcnt wait -- in the loader that
+// wait drains the whole in-flight weight stream.
+typedef const ENG_CONST EngArgs EngA;
+typedef const ENG_CONST EngLayer EngL;
+__device__ __forceinline__ EngLayer eng_layer(EngL &s) {
+	return EngLayer{s.wq, s.wk, s.wv, s.wo, s.w1, s.w2, s.w3, s.rms_att, s.rms_ffn, s.kc, s.vc};
+}
 
+// LDS: ring | part[ENG_MAXROWS][C] | ctl[ENG_CTL_WORDS] | prefetch landing pad (256 B, never read)
 template <int C>
 constexpr int eng_ring_slots() {
-	return (160 * 1024 - ENG_MAXROWS * C * 4 - ENG_CTL_WORDS * 4) / (ENG_IPS * ENG_ITEM);
+	return (160 * 1024 - ENG_MAXROWS * C * 4 - ENG_CTL_WORDS * 4 - ENG_PF_PAD) / (ENG_IPS * ENG_ITEM);
 }
 template <int C>
 constexpr size_t eng_lds_bytes() {
-	return (size_t)eng_ring_slots<C>() * ENG_IPS * ENG_ITEM + (size_t)ENG_MAXROWS * C * 4 + ENG_CTL_WORDS * 4;
+	return (size_t)eng_ring_slots<C>() * ENG_IPS * ENG_ITEM + (size_t)ENG_MAXROWS * C * 4 + ENG_CTL_WORDS * 4 +
+	       ENG_PF_PAD;
 }
 
 // ---------------------------------------------------------------- memory helpers
@@ -255,10 +274,11 @@ __device__ __forceinline__ float eng_sum4_t(const float (&v)[4]) {
 }
 
 // ---------------------------------------------------------------- phase geometry
-__device__ __forceinline__ int eng_kind(const EngArgs &a, int ph) {
+__device__ __forceinline__ int eng_kind(EngA &a, int ph) {
 	return ph < 5 * a.n_layers ? ph % 5 : EK_LOGITS;
 }
-__device__ __forceinline__ void eng_geo(const EngArgs &a, int kind, int &n, int &ngroups, int &R) {
+template <class A>
+__device__ __forceinline__ void eng_geo(const A &a, int kind, int &n, int &ngroups, int &R) {
 	switch (kind) {
 	case EK_QKV:
 		n = a.dim, ngroups = (a.q_dim + 2 * a.kv_dim) / 2, R = 2;
@@ -276,8 +296,13 @@ __device__ __forceinline__ void eng_geo(const EngArgs &a, int kind, int &n, int 
 		n = a.dim, ngroups = a.vocab, R = 1;
 	}
 }
+// the loader's phase geometry, copied into SGPRs once
+struct EngGeo {
+	int dim, hidden, q_dim, kv_dim, vocab;
+	const char *wcls;
+};
 template <class WT>
-__device__ __forceinline__ const char *eng_row(const EngArgs &a, const EngLayer &L, int kind, int g, int r, int n) {
+__device__ __forceinline__ const char *eng_row(const EngGeo &a, const EngLayer &L, int kind, int g, int r, int n) {
 	const size_t rb = (size_t)n * WT::BYTES;
 	switch (kind) {
 	case EK_QKV: {
@@ -328,37 +353,122 @@ __device__ __forceinline__ void eng_fail(unsigned *err, volatile ENG_LDS unsigne
 		__hip_atomic_fetch_or(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ring slots landed as a contiguous prefix: loader l's first missing slot is count_l * nl + l
+// (the NL <= 4 counters are one 16-byte LDS read)
+template <int NL>
+__device__ __forceinline__ unsigned eng_landed(volatile ENG_LDS unsigned *ctl, unsigned nl) {
+	static_assert(NL >= 1 && NL <= 4 && CTL_FULL % 4 == 0, "loader counters: one ds_read_b128");
+	const u32x4_t f = *(volatile ENG_LDS u32x4_t *)(ctl + CTL_FULL);
+	unsigned m = f[0] * nl;
+#pragma unroll
+	for (int l = 1; l < NL; ++l)
+		if (l < (int)nl)
+			m = min(m, f[l] * nl + l);
+	return m;
+}
+
+// ---------------------------------------------------------------- prefetch wave
+// 4-byte LDS-DMA per lane into the landing pad: the only purpose is the HBM read
+// it causes (the line lands in L2 / Infinity Cache); hipcc never sees the load.
+__device__ __forceinline__ void eng_touch(const void *g, unsigned pad_lds) {
+	unsigned keep;
+	asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+	             : "=&s"(keep)
+	             : "v"(g), "s"(pad_lds)
+	             : "memory");
+}
+// The loaders stop whenever the ring is full -- at every seam, while the consumers
+// wait for the other CUs -- and HBM idles until the consumers free slots. The
+// prefetch wave walks the same per-CU weight sequence up to pf_ahead items past
+// the landed ring and touches every 64-B line of it, so HBM keeps streaming
+// through the seams and the ring refills from on-die cache afterwards. Weights
+// are read-only: the prefetch changes timing only, never a value.
+template <class WT, int NL>
+__device__ __forceinline__ void eng_prefetch(EngA &ca, unsigned pad_lds, volatile ENG_LDS unsigned *ctl, int nl) {
+	const int b = blockIdx.x, NB = gridDim.x, lane = threadIdx.x & 63;
+	const EngGeo geo{ca.dim, ca.hidden, ca.q_dim, ca.kv_dim, ca.vocab, ca.wcls};
+	const int n_layers = ca.n_layers;
+	EngL *layers = (EngL *)ca.layers;
+	const int nph = 5 * n_layers + (ca.mode != EM_HYDRATE ? 1 : 0);
+	const unsigned ahead = (unsigned)ca.pf_ahead;
+	constexpr int TI = 64 * ENG_PF_LINE / ENG_ITEM; // items covered by one touch instruction
+	unsigned it = 0, lim = 0;                       // items walked / allowed
+	bool dead = false;
+	for (int ph = 0; ph < nph && !dead; ++ph) {
+		const int kind = ph < 5 * n_layers ? ph % 5 : EK_LOGITS;
+		if (kind == EK_ATTN)
+			continue;
+		const EngLayer Ly = eng_layer(layers[ph < 5 * n_layers ? ph / 5 : 0]);
+		int n, ngroups, R;
+		eng_geo(geo, kind, n, ngroups, R);
+		const int nch = n * WT::BYTES / ENG_ITEM;
+		const int ngl = eng_ngl(ngroups, b, NB);
+		for (int gl = 0; gl < ngl && !dead; ++gl) {
+			for (int r = 0; r < R && !dead; ++r) {
+				const char *rp = eng_row<WT>(geo, Ly, kind, b + gl * NB, r, n);
+				for (int c = 0; c < nch; c += TI) {
+					if (it + c >= lim) {
+						EngSpin sp;
+						while ((lim = eng_landed<NL>(ctl, nl) * ENG_IPS + ahead) <= it + c) {
+							if (eng_spin(sp, ctl)) { // loaders gone or stuck: stop prefetching, no error
+								dead = true;
+								break;
+							}
+						}
+						if (dead)
+							break;
+					}
+					const int off = c * ENG_ITEM + lane * ENG_PF_LINE;
+					if (off < nch * ENG_ITEM)
+						eng_touch(rp + off, pad_lds);
+					asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); // <= 33 x 4 KB in flight
+				}
+				it += nch;
+			}
+		}
+	}
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // ---------------------------------------------------------------- loader waves
 // L loader waves share the CU's item stream slot-interleaved: loader l issues the
 // 8 items of every slot s with s % L == l (one wave's DMA issue rate, ~8 GB/s,
 // is far below the CU's 25 GB/s share of HBM) and publishes how many of ITS
 // slots have landed (ctl[CTL_FULL + l]) behind its own counted vmcnt.
 template <class WT, int C, int NL>
-__device__ __forceinline__ void eng_loader(const EngArgs &a, unsigned ring_lds, volatile ENG_LDS unsigned *ctl, int l) {
+__device__ __forceinline__ void eng_loader(EngA &ca, unsigned ring_lds, volatile ENG_LDS unsigned *ctl, int l) {
 	constexpr int NS = eng_ring_slots<C>();
 	const int b = blockIdx.x, NB = gridDim.x, lane = threadIdx.x & 63;
-	const int nph = 5 * a.n_layers + (a.mode != EM_HYDRATE ? 1 : 0);
+	const EngGeo geo{ca.dim, ca.hidden, ca.q_dim, ca.kv_dim, ca.vocab, ca.wcls};
+	const int n_layers = ca.n_layers;
+	EngL *layers = (EngL *)ca.layers;
+	unsigned *const err = ca.err;
+	const int nph = 5 * n_layers + (ca.mode != EM_HYDRATE ? 1 : 0);
 	__builtin_amdgcn_s_setprio(3);
-	unsigned slot = 0, mine = 0, free_seen = NS, stall = 0;
-	const int depth = a.ld_depth;
-	const int nl = a.ld_waves;
-	if (l >= nl)
+	unsigned slot = 0, mine = 0, free_seen = NS, stall = 0, vmwait = 0;
+	const unsigned long long tbeg = __builtin_amdgcn_s_memrealtime();
+	const int depth = ca.ld_depth;
+	const int nl = ca.ld_waves;
+	if (l >= nl) {
+		if (l == nl && ca.pf_ahead > 0)
+			eng_prefetch<WT, NL>(ca, (unsigned)(uintptr_t)(ctl + ENG_CTL_WORDS), ctl, nl);
 		return;
-	const bool nt = a.ld_nt != 0;
+	}
+	const bool nt = ca.ld_nt != 0;
 	int k = 0; // items of the current slot already walked
 	bool dead = false;
 	for (int ph = 0; ph < nph && !dead; ++ph) {
-		const int kind = eng_kind(a, ph);
+		const int kind = ph < 5 * n_layers ? ph % 5 : EK_LOGITS;
 		if (kind == EK_ATTN)
 			continue;
-		const EngLayer &Ly = a.layers[ph < 5 * a.n_layers ? ph / 5 : 0];
+		const EngLayer Ly = eng_layer(layers[ph < 5 * n_layers ? ph / 5 : 0]);
 		int n, ngroups, R;
-		eng_geo(a, kind, n, ngroups, R);
+		eng_geo(geo, kind, n, ngroups, R);
 		const int nch = n * WT::BYTES / ENG_ITEM;
 		const int ngl = eng_ngl(ngroups, b, NB);
 		for (int gl = 0; gl < ngl && !dead; ++gl) {
 			for (int r = 0; r < R && !dead; ++r) {
-				const char *rp = eng_row<WT>(a, Ly, kind, b + gl * NB, r, n) + lane * 16;
+				const char *rp = eng_row<WT>(geo, Ly, kind, b + gl * NB, r, n) + lane * 16;
 				for (int c = 0; c < nch;) {
 					const int take = min(nch - c, ENG_IPS - k); // this row's items in the current slot
 					if ((int)(slot % nl) == l) {
@@ -374,7 +484,7 @@ __device__ __forceinline__ void eng_loader(const EngArgs &a, unsigned ring_lds, 
 								if (slot < free_seen)
 									break;
 								if (eng_spin(sp, ctl)) {
-									eng_fail(a.err, ctl, ENG_ERR_RING);
+									eng_fail(err, ctl, ENG_ERR_RING);
 									dead = true;
 									break;
 								}
@@ -392,7 +502,9 @@ __device__ __forceinline__ void eng_loader(const EngArgs &a, unsigned ring_lds, 
 					k += take;
 					if (k == ENG_IPS) {
 						if ((int)(slot % nl) == l && ++mine > (unsigned)depth) {
+							const unsigned long long tv = __builtin_amdgcn_s_memrealtime();
 							eng_vmcnt_slots(depth);
+							vmwait += (unsigned)(__builtin_amdgcn_s_memrealtime() - tv);
 							ctl[CTL_FULL + l] = mine - depth;
 						}
 						k = 0;
@@ -407,14 +519,18 @@ __device__ __forceinline__ void eng_loader(const EngArgs &a, unsigned ring_lds, 
 		++mine; // the partial last slot
 	ctl[CTL_FULL + l] = mine;
 	const unsigned long long tf = __builtin_amdgcn_s_memrealtime();
-	ctl[52] = (unsigned)tf;
-	ctl[53] = (unsigned)(tf >> 32);
+	if (l == 0) {
+		ctl[52] = (unsigned)tf;
+		ctl[53] = (unsigned)(tf >> 32);
+		ctl[54] = vmwait;              // ticks blocked in s_waitcnt vmcnt (data latency)
+		ctl[55] = (unsigned)(tf - tbeg); // loader 0 lifetime
+	}
 }
 
 // ---------------------------------------------------------------- consumer context
 template <class WT, int C, int NL>
 struct EngCtx {
-	const EngArgs &a;
+	EngA &a;
 	ENG_LDS char *ring;
 	ENG_LDS float *part;
 	volatile ENG_LDS unsigned *ctl;
@@ -423,7 +539,7 @@ struct EngCtx {
 	int token, pos, kv_sink, kv_pos, kv_len;
 	bool dead;
 
-	__device__ EngCtx(const EngArgs &a_) : a(a_) {}
+	__device__ EngCtx(EngA &a_) : a(a_) {}
 
 	// consumer-only barrier (the loader never joins: an s_barrier would stall its stream)
 	__device__ __forceinline__ void cbar() {
@@ -443,21 +559,7 @@ struct EngCtx {
 		}
 	}
 
-	// slots landed as a contiguous prefix: loader l's first missing slot is count_l * NL + l
-	// (the NL <= 4 counters are one 16-byte LDS read)
-	__device__ __forceinline__ unsigned landed() {
-		static_assert(NL >= 1 && NL <= 4 && CTL_FULL % 4 == 0, "loader counters: one ds_read_b128");
-		const u32x4_t f = *(volatile ENG_LDS u32x4_t *)(ctl + CTL_FULL);
-		const unsigned nl = (unsigned)a.ld_waves;
-		unsigned m = f[0] * nl;
-#pragma unroll
-		for (int l = 1; l < NL; ++l) {
-			const unsigned v = f[l];
-			if (l < (int)nl)
-				m = min(m, v * nl + l);
-		}
-		return m;
-	}
+	__device__ __forceinline__ unsigned landed() { return eng_landed<NL>(ctl, (unsigned)a.ld_waves); }
 	// ring slot holding item j has landed
 	__device__ __forceinline__ bool wait_item(unsigned j) {
 		const unsigned s = j / ENG_IPS;
@@ -467,6 +569,22 @@ struct EngCtx {
 		}
 		EngSpin sp;
 		while ((full_seen = landed()) <= s) {
+			switch (a.poll_sleep) { // extra back-off: every poll is an LDS op competing with the loaders' DMA issue
+			case 2:
+				__builtin_amdgcn_s_sleep(1);
+				break;
+			case 4:
+				__builtin_amdgcn_s_sleep(3);
+				break;
+			case 8:
+				__builtin_amdgcn_s_sleep(7);
+				break;
+			case 16:
+				__builtin_amdgcn_s_sleep(15);
+				break;
+			default:
+				break;
+			}
 			if (eng_spin(sp, ctl)) {
 				eng_fail(a.err, ctl, ENG_ERR_RING);
 				dead = true;
@@ -481,7 +599,8 @@ struct EngCtx {
 		return *(const ENG_LDS u32x4_t *)(ring + (size_t)(j % RING) * ENG_ITEM + lane * 16);
 	}
 	__device__ __forceinline__ void release(unsigned next_item) { // every lane stores the same word
-		eng_lds_rel(&ctl[CTL_CONS + w], next_item / ENG_IPS);
+		if (!(a.dbg & 128))
+			eng_lds_rel(&ctl[CTL_CONS + w], next_item / ENG_IPS);
 	}
 
 	// every CU finished phase `epoch` (flags are per-CU epochs, monotonic over launches)
@@ -578,7 +697,8 @@ __device__ __forceinline__ bool eng_rows(EngCtx<WT, C, NL> &cx, const float (&xr
 			acc[t] = a0 + a1;
 		}
 		const float tot = eng_sum4_t(acc);
-		cx.part[(r0 + (lane >> 4)) * C + w] = tot;
+		if (!(cx.a.dbg & 256))
+			cx.part[(r0 + (lane >> 4)) * C + w] = tot;
 	}
 	return true;
 }
@@ -589,8 +709,8 @@ __device__ __forceinline__ void eng_gemv(EngCtx<WT, C, NL> &cx, int kind, int la
 	constexpr int EPL = WT::EPL;
 	constexpr int KMAX = 64 / EPL; // x slice registers: KMAX x EPL = 64 floats per lane
 	constexpr int CH = 64 * EPL;   // elements per item
-	const EngArgs &a = cx.a;
-	const EngLayer &L = a.layers[kind == EK_LOGITS ? 0 : layer];
+	EngA &a = cx.a;
+	EngL &L = ((EngL *)a.layers)[kind == EK_LOGITS ? 0 : layer];
 	const int w = cx.w, lane = cx.lane;
 	int n, ngroups, R;
 	eng_geo(a, kind, n, ngroups, R);
@@ -602,9 +722,14 @@ __device__ __forceinline__ void eng_gemv(EngCtx<WT, C, NL> &cx, int kind, int la
 	const bool from_emb = kind == EK_QKV && layer == 0;
 	const float *xin = kind == EK_WO ? a.xb2 : (kind == EK_W2 ? a.hb : a.x);
 	const char *erow = a.emb + (size_t)cx.token * a.dim * WT::BYTES;
+	const bool gather = !(a.dbg & 64);
 #pragma unroll
 	for (int k = 0; k < KMAX; ++k) {
-		if (k < kw) {
+		if (k < kw && !gather) {
+#pragma unroll
+			for (int e = 0; e < EPL; ++e)
+				xr[k][e] = 0.0f;
+		} else if (k < kw) {
 			const int i0 = (w + k * C) * CH + lane * EPL;
 			if (from_emb) {
 				WT::unpack(load16(erow + (size_t)i0 * WT::BYTES), xr[k]);
@@ -616,7 +741,7 @@ __device__ __forceinline__ void eng_gemv(EngCtx<WT, C, NL> &cx, int kind, int la
 		}
 	}
 	// ---- rmsnorm (infer.cpp:134-144: scale = 1/sqrt(ss/n + eps); o = x * scale * w)
-	if (kind == EK_QKV || kind == EK_GLU || kind == EK_LOGITS) {
+	if (gather && (kind == EK_QKV || kind == EK_GLU || kind == EK_LOGITS)) {
 		const float *nw = kind == EK_QKV ? L.rms_att : (kind == EK_GLU ? L.rms_ffn : a.rms_final);
 		float ss = 0.0f;
 #pragma unroll
@@ -718,7 +843,7 @@ __device__ __forceinline__ void eng_gemv(EngCtx<WT, C, NL> &cx, int kind, int la
 	const int pos = cx.pos;
 	float best = -FLT_MAX;
 	int bi = 0x7fffffff;
-	for (int gl = cx.tid; gl < ngl && !cx.dead; gl += 64 * C) {
+	for (int gl = cx.tid; gl < ngl && !cx.dead && !(a.dbg & 32); gl += 64 * C) {
 		float acc[2];
 #pragma unroll
 		for (int r = 0; r < 2; ++r) {
@@ -808,7 +933,7 @@ __device__ __forceinline__ void eng_gemv(EngCtx<WT, C, NL> &cx, int kind, int la
 // kv head g, split s of S: chunks s, s + S, ... of ENG_KC keys. Lane layout: 16 lanes
 // per key row (8 dims each, D = 128), 4 rows per wave instruction, 8 rows per lane.
 template <int GT>
-__device__ __forceinline__ void eng_attn_unit(const EngArgs &a, const EngLayer &L, int g, int s, int S, int ns, int kv_len, int G,
+__device__ __forceinline__ void eng_attn_unit(EngA &a, EngL &L, int g, int s, int S, int ns, int kv_len, int G,
                               int lane, bool &dead, volatile ENG_LDS unsigned *ctl, int layer) {
 	constexpr int D = ENG_D;
 	const int sub = lane >> 4, piece = lane & 15;
@@ -981,7 +1106,7 @@ template <class WT, int C, int NL, int GT>
 __global__ __launch_bounds__(64 * (C + NL)) void engine_kernel(const EngArgs *__restrict__ args) {
 	// Arguments live in device memory (written once per decoder and mode): a
 	// by-value struct whose address is taken is copied to scratch per lane.
-	const EngArgs &a = *args;
+	EngA &a = *(EngA *)args;
 	extern __shared__ __attribute__((aligned(16))) char lds_raw[];
 	constexpr int NS = eng_ring_slots<C>();
 	ENG_LDS char *lds = (ENG_LDS char *)lds_raw;
@@ -1020,7 +1145,7 @@ __global__ __launch_bounds__(64 * (C + NL)) void engine_kernel(const EngArgs *__
 	cx.kv_pos = cx.kv_sink + (cx.pos - cx.kv_sink) % (a.max_seq_len - cx.kv_sink);
 	cx.kv_len = cx.pos >= a.max_seq_len ? a.max_seq_len : cx.pos + 1;
 
-	if ((a.dbg & 4) && cx.lane == 0) // timing only: the loaders stream unthrottled
+	if ((a.dbg & (4 | 128)) && cx.lane == 0) // timing only: the loaders stream unthrottled
 		ctl[CTL_CONS + cx.w] = 0x40000000u;
 	const int nph = 5 * a.n_layers + (a.mode != EM_HYDRATE ? 1 : 0);
 	unsigned long long *trb = a.trace && cx.w == 0 && cx.lane == 0 ? a.trace + (size_t)cx.b * E * 8 : nullptr;
@@ -1043,7 +1168,7 @@ __global__ __launch_bounds__(64 * (C + NL)) void engine_kernel(const EngArgs *__
 			const int G = a.n_heads / a.n_kv;
 			const int ns = (cx.kv_len + ENG_KC - 1) / ENG_KC;
 			const int S = min(ns, ENG_SMAX);
-			const EngLayer &L = a.layers[layer];
+			EngL &L = ((EngL *)a.layers)[layer];
 			for (int u = cx.b + cx.w * cx.NB; u < a.n_kv * S; u += cx.NB * C)
 				eng_attn_unit<GT>(a, L, u / S, u % S, S, ns, cx.kv_len, G, cx.lane, cx.dead, ctl, layer);
 			if (tr)
@@ -1061,6 +1186,8 @@ __global__ __launch_bounds__(64 * (C + NL)) void engine_kernel(const EngArgs *__
 		trb[(E - 1) * 8 + 1] = ctl[CTL_LSTALL];
 		trb[(E - 1) * 8 + 2] = (unsigned long long)ctl[52] | ((unsigned long long)ctl[53] << 32);
 		trb[(E - 1) * 8 + 3] = __builtin_amdgcn_s_memrealtime();
+		trb[(E - 1) * 8 + 4] = ctl[54];
+		trb[(E - 1) * 8 + 5] = ctl[55];
 	}
 	if (cx.dead)
 		return;

@@ -97,8 +97,13 @@ int engine_init(yalm_decoder_s *d) {
 	const int depth = depth_env ? std::max(1, std::min(7, atoi(depth_env))) : ENG_LD;
 	const char *nt_env = getenv("YALM_ENGINE_NT");
 	const int ld_nt = nt_env ? atoi(nt_env) != 0 : 1;
+	const char *pf_env = getenv("YALM_ENGINE_PF"); // KB of prefetch run-ahead; > 0 turns the last loader wave into the prefetcher
+	const int pf_kb = pf_env ? std::max(0, atoi(pf_env)) : 0;
 	const char *lw_env = getenv("YALM_ENGINE_LOADERS");
-	const int ld_waves = lw_env ? std::max(1, std::min(ENG_L, atoi(lw_env))) : ENG_L;
+	const int ld_max = pf_kb > 0 ? ENG_L - 1 : ENG_L;
+	const int ld_waves = lw_env ? std::max(1, std::min(ld_max, atoi(lw_env))) : ld_max;
+	const char *sl_env = getenv("YALM_ENGINE_SLEEP");
+	const int poll_sleep = sl_env ? atoi(sl_env) : 1;
 
 	EngArgs a[N_GRAPHS];
 	for (int which = 0; which < N_GRAPHS; ++which) {
@@ -140,6 +145,8 @@ int engine_init(yalm_decoder_s *d) {
 		e.ld_depth = depth;
 		e.ld_nt = ld_nt;
 		e.ld_waves = ld_waves;
+		e.poll_sleep = poll_sleep;
+		e.pf_ahead = pf_kb * 1024 / ENG_ITEM;
 	}
 	HIPCHK(hipMemcpy(d->eng_args, a, sizeof(a), hipMemcpyHostToDevice));
 	d->eng_nb = nb;
