@@ -154,6 +154,12 @@ const char *yalm_kernel_name(yalm_decoder d, int kernel_id);
  * engine is opt-in, YALM_ENGINE=1).
  * yalm_time_kernel(d, 6, ...) times one greedy engine launch. */
 int yalm_decoder_engine(yalm_decoder d);
+/* 1 if this decoder's launch path runs attention and the Wo projection (+ the
+ * residual add) as ONE launch (attn_wo.h: the Wo weight stream overlaps the
+ * attention; replaces attn + fused_matmul_add_residuals, infer.cu:338-524, 270):
+ * single GPU, head_dim 128, fp16 / fp8 weights with 4 or 8 KB Wo rows, and
+ * YALM_ATTN_WO not 0 at creation. 0 = two separate launches. */
+int yalm_decoder_attn_wo(yalm_decoder d);
 /* Timeline of the engine's most recent launch (decoder created with
  * YALM_ENGINE_TRACE=1): for workgroup w and phase p (5 per layer: QKV,
  * attention, Wo, W1/W3, W2; then logits; the last index 5 L + 1 holds per-CU

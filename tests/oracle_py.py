@@ -167,8 +167,11 @@ class OracleModel:
         emb = self.t["model.embed.weight"]
         wcls = self.t.get("model.output.weight", emb)
         self.om = OModel(self.oc, P(emb), P(self.t["model.norm.weight"]), P(wcls), self.blocks)
+        # xb2 holds the attention output (q_dim floats) and later the W2 output
+        # (dim): the reference sizes it dim (its models have q_dim == dim)
         self.buf = {
-            "x": np.zeros(c.dim, np.float32), "xb": np.zeros(c.dim, np.float32), "xb2": np.zeros(c.dim, np.float32),
+            "x": np.zeros(c.dim, np.float32), "xb": np.zeros(c.dim, np.float32),
+            "xb2": np.zeros(max(c.dim, c.q_dim), np.float32),
             "hb": np.zeros(c.hidden_dim, np.float32), "hb2": np.zeros(c.hidden_dim, np.float32),
             "q": np.zeros(c.q_dim, np.float32), "k": np.zeros(c.kv_dim, np.float32),
             "v": np.zeros(c.kv_dim, np.float32), "att": np.zeros(c.n_heads * c.max_seq_len, np.float32),

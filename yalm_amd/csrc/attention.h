@@ -46,12 +46,29 @@ __device__ __forceinline__ float ld_sc1(const float *p) {
 	return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// head outputs: plain stores for the next launch, write-through (sc1) when other
+// workgroups of the same launch read them (attn_wo.h)
+template <bool SC1>
+__device__ __forceinline__ void attn_out(float *p, float v) {
+	if constexpr (SC1)
+		st_sc1(p, v);
+	else
+		*p = v;
+}
+
+// One workgroup's share of the split-KV attention: kv head g, key chunks s0,
+// s0 + S, ... `hook()` runs right after the speculative K/V and q loads are
+// issued (attn_wo.h issues its weight stream there, behind them in vmcnt order).
+// Returns true on the workgroup that wrote the final head outputs of kv head g
+// (the single-chunk writer or the last arriver); the result is workgroup-uniform.
 // D = head_dim (multiple of 8, D/8 a power of two <= 64); GT >= G.
-template <int D, int GT>
-__global__ __launch_bounds__(ATTN_THREADS) void attn_decode_kernel(
-    const float *__restrict__ q, const uint16_t *__restrict__ kc, const uint16_t *__restrict__ vc,
-    const StepState *__restrict__ step, int n_heads, int n_kv_heads, int max_seq_len, int nsplit,
-    float *__restrict__ part, unsigned *__restrict__ counters, float *__restrict__ out, float *__restrict__ att_dbg) {
+template <int D, int GT, bool SC1OUT, class Hook>
+// (no __restrict__ here: with it the K/V and q loads may legally sink below the
+// hook's asm barrier once inlined; the standalone kernel keeps it on its arguments)
+__device__ __forceinline__ bool attn_decode_body(bool active, int g, int s0, int S, const float *q, const uint16_t *kc,
+                                                 const uint16_t *vc, const StepState *step, int n_heads,
+                                                 int n_kv_heads, int max_seq_len, int nsplit, float *part,
+                                                 unsigned *counters, float *out, float *att_dbg, Hook &&hook) {
 	constexpr int CHUNK = attn_chunk<D>();
 	constexpr int LPK = D / 8;                     // lanes per K/V row, 16 B each
 	constexpr int KPW = 64 / LPK;                  // rows per wave-instruction
@@ -63,9 +80,6 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_decode_kernel(
 	__shared__ float ml[GT][2];
 	__shared__ int last_flag;
 
-	const int g = blockIdx.x;
-	const int s0 = blockIdx.y;
-	const int S = gridDim.y;
 	const int G = n_heads / n_kv_heads;
 	const int kv_dim = n_kv_heads * D;
 	const int lane = threadIdx.x & 63;
@@ -97,9 +111,10 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_decode_kernel(
 		qr[h][0] = a[0], qr[h][1] = a[1], qr[h][2] = a[2], qr[h][3] = a[3];
 		qr[h][4] = b[0], qr[h][5] = b[1], qr[h][6] = b[2], qr[h][7] = b[3];
 	}
-	const int kv_len = step->kv_len;
-	if (s0 * CHUNK >= kv_len)
-		return; // whole workgroup exits before any barrier
+	const int kv_len = step->kv_len; // issued before the hook's loads: its wait must not cover them
+	hook();
+	if (!active || s0 * CHUNK >= kv_len)
+		return false; // whole workgroup leaves before any barrier
 	const int ns = (kv_len + CHUNK - 1) / CHUNK;
 	const float sq = sqrtf((float)D);
 
@@ -211,7 +226,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_decode_kernel(
 #pragma unroll
 				for (int w = 0; w < ATTN_WAVES * KPW; ++w)
 					o += red[w][h][d];
-				out[(size_t)(g * G + h) * D + d] = o / ml[h][1];
+				attn_out<SC1OUT>(out + (size_t)(g * G + h) * D + d, o / ml[h][1]);
 			}
 			if (att_dbg) {
 				for (int i = tid; i < G * nt; i += ATTN_THREADS) {
@@ -219,7 +234,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_decode_kernel(
 					att_dbg[(size_t)(g * G + h) * max_seq_len + t] = sc[h][t] / ml[h][1];
 				}
 			}
-			return;
+			return true;
 		}
 
 		// ---- publish this chunk's partial (o[D], m, l per head) write-through
@@ -250,7 +265,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_decode_kernel(
 	}
 	__syncthreads();
 	if (!last_flag)
-		return;
+		return false;
 
 	// ---- last arriver: merge the ns chunk partials of heads g*G .. in chunk order.
 	// Batches of MB chunks: every (m, l, o[d]) load of a batch is issued before any
@@ -302,7 +317,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_decode_kernel(
 		if (dl) {
 #pragma unroll
 			for (int k = 0; k < DPL; ++k)
-				out[(size_t)(g * G + h) * D + lane + 64 * k] = o[k] / L;
+				attn_out<SC1OUT>(out + (size_t)(g * G + h) * D + lane + 64 * k, o[k] / L);
 		}
 		if (att_dbg) {
 			for (int t = lane; t < kv_len; t += 64) {
@@ -311,4 +326,14 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_decode_kernel(
 			}
 		}
 	}
+	return true;
+}
+
+template <int D, int GT>
+__global__ __launch_bounds__(ATTN_THREADS) void attn_decode_kernel(
+    const float *__restrict__ q, const uint16_t *__restrict__ kc, const uint16_t *__restrict__ vc,
+    const StepState *__restrict__ step, int n_heads, int n_kv_heads, int max_seq_len, int nsplit,
+    float *__restrict__ part, unsigned *__restrict__ counters, float *__restrict__ out, float *__restrict__ att_dbg) {
+	attn_decode_body<D, GT, false>(true, blockIdx.x, blockIdx.y, gridDim.y, q, kc, vc, step, n_heads, n_kv_heads, max_seq_len,
+	                               nsplit, part, counters, out, att_dbg, [] {});
 }

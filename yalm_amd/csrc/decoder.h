@@ -120,6 +120,13 @@ struct yalm_decoder_s {
 	float *eng_amax = nullptr;       // [NB][2] per-CU (max, index)
 	EngArgs *eng_args = nullptr;     // [N_GRAPHS] kernel arguments per mode (device)
 	unsigned long long *eng_trace = nullptr; // YALM_ENGINE_TRACE=1: [NB][5 L + 2][8] stamps
+	// launch path: attention + Wo as one launch (attn_wo.h) when supported;
+	// YALM_ATTN_WO=0 selects the two separate kernels
+	bool attn_wo = false;
+	int awo_nb = 0;                  // grid: n_kv * awo_S attention + ceil(dim / AWO_RPW) Wo workgroups
+	int awo_S = 0;                   // key-chunk splits per kv head
+	unsigned *awo_sync = nullptr;    // [n_layers][AWO_SLOT] done counters, then the error word
+	unsigned *awo_err = nullptr;     // = awo_sync + n_layers * AWO_SLOT
 };
 
 // ------------------------------------------------------------------ shared helpers

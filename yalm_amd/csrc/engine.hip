@@ -183,6 +183,15 @@ int engine_enqueue(yalm_decoder_s *d, int which) {
 
 // After a stream sync: the engine's bounded spins report here instead of hanging.
 int engine_check(yalm_decoder_s *d) {
+	if (d->awo_err) { // the fused attention + Wo launch spins too (attn_wo.h)
+		unsigned e = 0;
+		HIPCHK(hipMemcpy(&e, d->awo_err, sizeof(e), hipMemcpyDeviceToHost));
+		if (e) {
+			set_err("fused attention + Wo launch gave up waiting for the attention heads (error bits " +
+			        std::to_string(e) + "): grid not co-resident; YALM_ATTN_WO=0 selects separate launches");
+			return YALM_ERR_HIP;
+		}
+	}
 	if (!d->engine)
 		return YALM_OK;
 	unsigned e = 0;

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "attention.h"
+#include "attn_wo.h"
 #include "decoder.h"
 #include "device_common.h"
 #include "gemv.h"
@@ -355,6 +356,99 @@ static int launch_attn(int head_dim, int n_heads, int n_kv, const float *q, cons
 	return YALM_OK;
 }
 
+// ---- attention + Wo in one launch (attn_wo.h)
+template <class WT, int GT, int XS>
+static const void *attn_wo_fn() {
+	return (const void *)attn_wo_kernel<WT, GT, XS>;
+}
+template <class WT, int XS>
+static const void *attn_wo_fn_g(int G) {
+	return G <= 1 ? attn_wo_fn<WT, 1, XS>() : G <= 2 ? attn_wo_fn<WT, 2, XS>() : G <= 4 ? attn_wo_fn<WT, 4, XS>()
+	                                                                         : attn_wo_fn<WT, 8, XS>();
+}
+static const void *attn_wo_pick(int dtype, int G, int XS) {
+	if (dtype == YALM_F16)
+		return XS == 1 ? attn_wo_fn_g<WF16, 1>(G) : attn_wo_fn_g<WF16, 2>(G);
+	return XS == 1 ? attn_wo_fn_g<WF8, 1>(G) : attn_wo_fn_g<WF8, 2>(G);
+}
+
+// Single-GPU decoders with head_dim 128, G <= 8, fp16 / fp8 Wo rows of 4 or 8 KB and
+// at least 2 layers (layer l zeroes layer l - 1's hand-off counter).
+static int attn_wo_init(yalm_decoder_s *d) {
+	const yalm_config &c = d->c;
+	const char *env = getenv("YALM_ATTN_WO");
+	if (env && atoi(env) == 0)
+		return YALM_OK;
+	if (d->comm || d->ipc || d->tp_size > 1 || c.head_dim != 128)
+		return YALM_OK;
+	const int G = c.n_heads / c.n_kv_heads;
+	if (G < 1 || G > 8 || (c.weight_dtype != YALM_F16 && c.weight_dtype != YALM_F8E5M2))
+		return YALM_OK;
+	const int rb = c.n_heads * c.head_dim * (c.weight_dtype == YALM_F16 ? 2 : 1);
+	if (rb != 4096 && rb != 8192)
+		return YALM_OK;
+	if (c.dim < AWO_RPW || c.n_layers < 2)
+		return YALM_OK;
+	int occ = 0; // the Wo workgroups spin, but only on attention workgroups dispatched before them
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, attn_wo_pick(c.weight_dtype, G, rb / 4096), ATTN_THREADS,
+	                                                 0) != hipSuccess ||
+	    occ < 1)
+		return YALM_OK;
+	const int nchunks = (c.max_seq_len + attn_chunk<128>() - 1) / attn_chunk<128>();
+	// per layer AWO_SLOT words (8 counter replicas on lines of their own), then the error word
+	TRY(dalloc(d, (void **)&d->awo_sync, sizeof(unsigned) * ((size_t)c.n_layers * AWO_SLOT + AWO_REPL_STRIDE)));
+	d->awo_err = d->awo_sync + (size_t)c.n_layers * AWO_SLOT;
+	d->awo_S = std::min(nchunks, 32); // key-chunk splits per kv head, as the standalone attention launch
+	d->awo_nb = c.n_kv_heads * d->awo_S + (c.dim + AWO_RPW - 1) / AWO_RPW;
+	d->attn_wo = true;
+	return YALM_OK;
+}
+
+template <class WT, int GT, int XS>
+static void launch_attn_wo_k(yalm_decoder_s *d, const yalm_block_weights &w, const AttnWoArgs &p) {
+	attn_wo_kernel<WT, GT, XS><<<d->awo_nb, ATTN_THREADS, 0, d->stream>>>(d->q, w.key_cache, w.value_cache, d->step, p);
+}
+template <class WT, int XS>
+static void launch_attn_wo_g(yalm_decoder_s *d, const yalm_block_weights &w, const AttnWoArgs &p, int G) {
+	if (G <= 1)
+		launch_attn_wo_k<WT, 1, XS>(d, w, p);
+	else if (G <= 2)
+		launch_attn_wo_k<WT, 2, XS>(d, w, p);
+	else if (G <= 4)
+		launch_attn_wo_k<WT, 4, XS>(d, w, p);
+	else
+		launch_attn_wo_k<WT, 8, XS>(d, w, p);
+}
+template <class WT>
+static int launch_attn_wo(yalm_decoder_s *d, const yalm_block_weights &w, int layer) {
+	const yalm_config &c = d->c;
+	AttnWoArgs p;
+	p.n_heads = c.n_heads;
+	p.n_kv = c.n_kv_heads;
+	p.max_seq_len = c.max_seq_len;
+	p.nsplit = attn_nsplit(c.max_seq_len);
+	p.S = d->awo_S;
+	p.q_dim = c.n_heads * c.head_dim;
+	p.dim = c.dim;
+	p.part = d->part;
+	p.counters = d->attn_counters;
+	p.att = d->xb2;
+	p.wo = (const char *)w.wo;
+	p.x = d->x;
+	p.done = d->awo_sync + (size_t)layer * AWO_SLOT;
+	p.prev = d->awo_sync + (size_t)((layer + c.n_layers - 1) % c.n_layers) * AWO_SLOT;
+	p.err = d->awo_err;
+	const int G = c.n_heads / c.n_kv_heads;
+	if constexpr (WT::BYTES == 2 || WT::BYTES == 1) {
+		if (p.q_dim * WT::BYTES == 4096)
+			launch_attn_wo_g<WT, 1>(d, w, p, G);
+		else
+			launch_attn_wo_g<WT, 2>(d, w, p, G);
+	}
+	HIPCHK(hipGetLastError());
+	return YALM_OK;
+}
+
 static const unsigned *ipc_seq(const yalm_decoder_s *d) {
 	return (const unsigned *)(d->ipc_own + 2 * (size_t)d->ipc_S) + 64;
 }
@@ -439,11 +533,15 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 		p.vcache = w.value_cache;
 		TRY((launch_gemv<WT, PQKV<WT>, true>(p, d->x, w.rms_att, c.norm_eps, GK_QKV, d->gemv[GK_QKV], st)));
 	}
-	if (!(ab & 2))
-		TRY(launch_attn(c.head_dim, c.n_heads, c.n_kv_heads, d->q, w.key_cache, w.value_cache, d->step,
-		                c.max_seq_len, d->part, d->attn_counters, nullptr, d->xb2, st));
-	if (!(ab & 4))
-		TRY(enqueue_residual_gemv<WT>(d, w.wo, q_dim, d->xb2, GK_WO));
+	if (d->attn_wo && WT::BYTES <= 2 && !(ab & 6)) {
+		TRY(launch_attn_wo<WT>(d, w, l));
+	} else {
+		if (!(ab & 2))
+			TRY(launch_attn(c.head_dim, c.n_heads, c.n_kv_heads, d->q, w.key_cache, w.value_cache, d->step,
+			                c.max_seq_len, d->part, d->attn_counters, nullptr, d->xb2, st));
+		if (!(ab & 4))
+			TRY(enqueue_residual_gemv<WT>(d, w.wo, q_dim, d->xb2, GK_WO));
+	}
 	if (ab & 8) {
 	} else if (c.act == YALM_SILU) {
 		PGlu<WT, 1> p;
@@ -715,7 +813,7 @@ static int create_decoder(const yalm_config *config, const yalm_model_weights *w
 		set_err("hipHostMalloc failed");
 		return fail(YALM_ERR_HIP);
 	}
-	if ((r = engine_init(d)))
+	if ((r = engine_init(d)) || (r = attn_wo_init(d)))
 		return fail(r);
 	if (hipDeviceSynchronize() != hipSuccess) {
 		set_err("hipDeviceSynchronize failed after decoder allocation");
@@ -1010,6 +1108,10 @@ static int enqueue_one_t(yalm_decoder_s *d, int kernel_id, int l) {
 
 extern "C" int yalm_decoder_engine(yalm_decoder d) {
 	return d && d->engine ? 1 : 0;
+}
+
+extern "C" int yalm_decoder_attn_wo(yalm_decoder d) {
+	return d && d->attn_wo ? 1 : 0;
 }
 
 extern "C" int yalm_time_kernel(yalm_decoder d, int kernel_id, int iters, float *avg_ms) {

@@ -105,6 +105,7 @@ _sig("yalm_time_kernel", c_int, [c_void_p, c_int, c_int, ctypes.POINTER(c_float)
 _sig("yalm_kernel_name", ctypes.c_char_p, [c_void_p, c_int])
 _sig("yalm_set_gemv_config", c_int, [c_void_p, c_int, c_int, c_int, c_int])
 _sig("yalm_decoder_engine", c_int, [c_void_p])
+_sig("yalm_decoder_attn_wo", c_int, [c_void_p])
 _sig("yalm_engine_trace", c_int, [c_void_p, c_void_p, ctypes.c_size_t, ctypes.POINTER(c_int)])
 _sig("yalm_matmul", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int])
 _sig("yalm_mha", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int])
@@ -127,7 +128,7 @@ EXPORTED = [
     "yalm_time_kernel", "yalm_kernel_name", "yalm_set_gemv_config", "yalm_matmul", "yalm_mha", "yalm_ffn",
     "yalm_prefill", "yalm_prefill_time", "yalm_gemm_f16", "yalm_attn_prefill", "yalm_tp_unique_id",
     "yalm_decoder_create_tp", "yalm_copy_2d", "yalm_tp_ipc_alloc", "yalm_decoder_create_tp_ipc",
-    "yalm_decoder_engine", "yalm_engine_trace",
+    "yalm_decoder_engine", "yalm_engine_trace", "yalm_decoder_attn_wo",
 ]
 
 HYDRATE_KV_CACHE, OUTPUT_LOGITS = 0, 1
@@ -422,6 +423,11 @@ class Decoder:
     def engine(self) -> bool:
         """True when each token runs as one persistent engine launch (engine.h)."""
         return bool(lib.yalm_decoder_engine(self.h))
+
+    @property
+    def attn_wo(self) -> bool:
+        """True when the launch path runs attention + Wo as one launch (attn_wo.h)."""
+        return bool(lib.yalm_decoder_attn_wo(self.h))
 
     def engine_trace(self) -> np.ndarray:
         """(workgroups, 5 L + 2, 8) uint64 timeline of the last engine launch
