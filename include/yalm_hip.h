@@ -160,6 +160,13 @@ int yalm_decoder_engine(yalm_decoder d);
  * single GPU, head_dim 128, fp16 / fp8 weights with 4 or 8 KB Wo rows, and
  * YALM_ATTN_WO not 0 at creation. 0 = two separate launches. */
 int yalm_decoder_attn_wo(yalm_decoder d);
+/* Timeline of the most recent fused attention + Wo launch (decoder created with
+ * YALM_ATTN_WO_TRACE=1): 4 s_memrealtime (100 MHz) stamps per workgroup at
+ * [w * 4 + k]: start, hand-off signalled (attention; 0 if this workgroup did not
+ * finish a kv head) or Wo slice issued (Wo), poll passed (Wo), end. Workgroups
+ * [0, *attention_workgroups) are attention, the rest Wo. */
+int yalm_attn_wo_trace(yalm_decoder d, unsigned long long *host, size_t count, int *workgroups,
+                       int *attention_workgroups);
 /* Timeline of the engine's most recent launch (decoder created with
  * YALM_ENGINE_TRACE=1): for workgroup w and phase p (5 per layer: QKV,
  * attention, Wo, W1/W3, W2; then logits; the last index 5 L + 1 holds per-CU

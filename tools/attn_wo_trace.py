@@ -1,0 +1,58 @@
+"""Timeline of the fused attention + Wo launch (attn_wo.h) on a Mistral-7B-shaped
+synthetic model: the last layer's launch of the last token, from the
+per-workgroup s_memrealtime stamps (100 MHz) of yalm_attn_wo_trace.
+
+usage: python tools/attn_wo_trace.py [--model mistral-7b] [--ctx 150]
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ["YALM_ATTN_WO_TRACE"] = "1"
+
+from yalm_amd import models as M  # noqa: E402
+from yalm_amd import runtime  # noqa: E402
+
+
+def q(v):
+    return f"min {v.min():6.2f} med {np.median(v):6.2f} max {v.max():6.2f}"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="mistral-7b")
+    ap.add_argument("--ctx", type=int, default=150)
+    args = ap.parse_args()
+    runtime.check(runtime.lib.yalm_set_device(0))
+    cfg = M.PRESETS[args.model].with_(weight_dtype=M.F16)
+    dm = runtime.DeviceModel.synthetic(cfg, seed=1)
+    dec = runtime.Decoder(dm)
+    assert dec.attn_wo, "decoder does not run the fused attention + Wo launch"
+    for pos in range(args.ctx):
+        dec.forward((7 * pos + 1) % cfg.vocab_size, pos, runtime.HYDRATE_KV_CACHE)
+    dec.forward(5, args.ctx)
+    tr, na = dec.attn_wo_trace()
+    tr = tr.astype(np.int64)
+    t0 = tr[:, 0].min()
+    us = (tr - t0) / 100.0
+    att, wo = us[:na], us[na:]
+    writers = att[tr[:na, 1] > 0]
+    print(f"[{args.model} kv_len {args.ctx + 1}] grid {len(tr)} = {na} attention + {len(tr) - na} Wo workgroups; "
+          f"launch span {us[:, 3].max():.2f} us")
+    print(f"attention start  {q(att[:, 0])}")
+    print(f"attention end    {q(att[:, 3])}")
+    print(f"head signalled   {q(writers[:, 1])}  ({len(writers)} writers)")
+    print(f"Wo start         {q(wo[:, 0])}")
+    print(f"Wo slice issued  {q(wo[:, 1])}")
+    print(f"Wo poll passed   {q(wo[:, 2])}")
+    print(f"Wo end           {q(wo[:, 3])}")
+    dec.close()
+    dm.close()
+
+
+if __name__ == "__main__":
+    main()

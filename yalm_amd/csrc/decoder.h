@@ -125,8 +125,9 @@ struct yalm_decoder_s {
 	bool attn_wo = false;
 	int awo_nb = 0;                  // grid: n_kv * awo_S attention + ceil(dim / AWO_RPW) Wo workgroups
 	int awo_S = 0;                   // key-chunk splits per kv head
-	unsigned *awo_sync = nullptr;    // [n_layers][AWO_SLOT] done counters, then the error word
-	unsigned *awo_err = nullptr;     // = awo_sync + n_layers * AWO_SLOT
+	unsigned long long *awo_trace = nullptr; // YALM_ATTN_WO_TRACE=1: [grid][4] stamps of the last launch
+	unsigned *awo_sync = nullptr;    // [n_layers][n_kv][AWO_HEAD] per-kv-head done counters, then the error word
+	unsigned *awo_err = nullptr;     // = awo_sync + n_layers * n_kv * AWO_HEAD
 };
 
 // ------------------------------------------------------------------ shared helpers

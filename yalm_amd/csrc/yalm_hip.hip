@@ -387,7 +387,7 @@ static int attn_wo_init(yalm_decoder_s *d) {
 	const int rb = c.n_heads * c.head_dim * (c.weight_dtype == YALM_F16 ? 2 : 1);
 	if (rb != 4096 && rb != 8192)
 		return YALM_OK;
-	if (c.dim < AWO_RPW || c.n_layers < 2)
+	if (c.dim < AWO_RPW || c.n_layers < 2 || c.n_kv_heads * AWO_REPL > ATTN_THREADS)
 		return YALM_OK;
 	int occ = 0; // the Wo workgroups spin, but only on attention workgroups dispatched before them
 	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, attn_wo_pick(c.weight_dtype, G, rb / 4096), ATTN_THREADS,
@@ -395,11 +395,14 @@ static int attn_wo_init(yalm_decoder_s *d) {
 	    occ < 1)
 		return YALM_OK;
 	const int nchunks = (c.max_seq_len + attn_chunk<128>() - 1) / attn_chunk<128>();
-	// per layer AWO_SLOT words (8 counter replicas on lines of their own), then the error word
-	TRY(dalloc(d, (void **)&d->awo_sync, sizeof(unsigned) * ((size_t)c.n_layers * AWO_SLOT + AWO_REPL_STRIDE)));
-	d->awo_err = d->awo_sync + (size_t)c.n_layers * AWO_SLOT;
+	const size_t slot = (size_t)c.n_kv_heads * AWO_HEAD; // per layer: one counter per kv head
+	TRY(dalloc(d, (void **)&d->awo_sync, sizeof(unsigned) * (c.n_layers * slot + AWO_REPL_STRIDE)));
+	d->awo_err = d->awo_sync + c.n_layers * slot;
 	d->awo_S = std::min(nchunks, 32); // key-chunk splits per kv head, as the standalone attention launch
 	d->awo_nb = c.n_kv_heads * d->awo_S + (c.dim + AWO_RPW - 1) / AWO_RPW;
+	const char *tenv = getenv("YALM_ATTN_WO_TRACE");
+	if (tenv && atoi(tenv) != 0)
+		TRY(dalloc(d, (void **)&d->awo_trace, sizeof(unsigned long long) * 4 * d->awo_nb));
 	d->attn_wo = true;
 	return YALM_OK;
 }
@@ -435,9 +438,11 @@ static int launch_attn_wo(yalm_decoder_s *d, const yalm_block_weights &w, int la
 	p.att = d->xb2;
 	p.wo = (const char *)w.wo;
 	p.x = d->x;
-	p.done = d->awo_sync + (size_t)layer * AWO_SLOT;
-	p.prev = d->awo_sync + (size_t)((layer + c.n_layers - 1) % c.n_layers) * AWO_SLOT;
+	const size_t slot = (size_t)c.n_kv_heads * AWO_HEAD;
+	p.done = d->awo_sync + (size_t)layer * slot;
+	p.prev = d->awo_sync + (size_t)((layer + c.n_layers - 1) % c.n_layers) * slot;
 	p.err = d->awo_err;
+	p.trace = d->awo_trace;
 	const int G = c.n_heads / c.n_kv_heads;
 	if constexpr (WT::BYTES == 2 || WT::BYTES == 1) {
 		if (p.q_dim * WT::BYTES == 4096)
@@ -1112,6 +1117,20 @@ extern "C" int yalm_decoder_engine(yalm_decoder d) {
 
 extern "C" int yalm_decoder_attn_wo(yalm_decoder d) {
 	return d && d->attn_wo ? 1 : 0;
+}
+
+extern "C" int yalm_attn_wo_trace(yalm_decoder d, unsigned long long *host, size_t count, int *workgroups,
+                                  int *attention_workgroups) {
+	ARGCHK(d && host, "null argument");
+	ARGCHK(d->attn_wo && d->awo_trace, "no attn_wo trace (create the decoder with YALM_ATTN_WO_TRACE=1)");
+	HIPCHK(hipStreamSynchronize(d->stream));
+	const size_t total = (size_t)4 * d->awo_nb;
+	HIPCHK(hipMemcpy(host, d->awo_trace, sizeof(unsigned long long) * std::min(count, total), hipMemcpyDeviceToHost));
+	if (workgroups)
+		*workgroups = d->awo_nb;
+	if (attention_workgroups)
+		*attention_workgroups = d->c.n_kv_heads * d->awo_S;
+	return YALM_OK;
 }
 
 extern "C" int yalm_time_kernel(yalm_decoder d, int kernel_id, int iters, float *avg_ms) {

@@ -106,6 +106,7 @@ _sig("yalm_kernel_name", ctypes.c_char_p, [c_void_p, c_int])
 _sig("yalm_set_gemv_config", c_int, [c_void_p, c_int, c_int, c_int, c_int])
 _sig("yalm_decoder_engine", c_int, [c_void_p])
 _sig("yalm_decoder_attn_wo", c_int, [c_void_p])
+_sig("yalm_attn_wo_trace", c_int, [c_void_p, c_void_p, ctypes.c_size_t, ctypes.POINTER(c_int), ctypes.POINTER(c_int)])
 _sig("yalm_engine_trace", c_int, [c_void_p, c_void_p, ctypes.c_size_t, ctypes.POINTER(c_int)])
 _sig("yalm_matmul", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int])
 _sig("yalm_mha", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int])
@@ -128,7 +129,7 @@ EXPORTED = [
     "yalm_time_kernel", "yalm_kernel_name", "yalm_set_gemv_config", "yalm_matmul", "yalm_mha", "yalm_ffn",
     "yalm_prefill", "yalm_prefill_time", "yalm_gemm_f16", "yalm_attn_prefill", "yalm_tp_unique_id",
     "yalm_decoder_create_tp", "yalm_copy_2d", "yalm_tp_ipc_alloc", "yalm_decoder_create_tp_ipc",
-    "yalm_decoder_engine", "yalm_engine_trace", "yalm_decoder_attn_wo",
+    "yalm_decoder_engine", "yalm_engine_trace", "yalm_decoder_attn_wo", "yalm_attn_wo_trace",
 ]
 
 HYDRATE_KV_CACHE, OUTPUT_LOGITS = 0, 1
@@ -428,6 +429,14 @@ class Decoder:
     def attn_wo(self) -> bool:
         """True when the launch path runs attention + Wo as one launch (attn_wo.h)."""
         return bool(lib.yalm_decoder_attn_wo(self.h))
+
+    def attn_wo_trace(self):
+        """((workgroups, 4) uint64 stamps, attention workgroups) of the last fused
+        attention + Wo launch (decoder created with YALM_ATTN_WO_TRACE=1)."""
+        buf = np.zeros(4 * 8192, np.uint64)
+        nb, na = c_int(), c_int()
+        check(lib.yalm_attn_wo_trace(self.h, buf.ctypes.data, buf.size, ctypes.byref(nb), ctypes.byref(na)))
+        return buf[: 4 * nb.value].reshape(nb.value, 4), na.value
 
     def engine_trace(self) -> np.ndarray:
         """(workgroups, 5 L + 2, 8) uint64 timeline of the last engine launch
