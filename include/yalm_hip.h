@@ -163,7 +163,7 @@ int yalm_decoder_attn_wo(yalm_decoder d);
 /* Timeline of the most recent fused attention + Wo launch (decoder created with
  * YALM_ATTN_WO_TRACE=1): 4 s_memrealtime (100 MHz) stamps per workgroup at
  * [w * 4 + k]: start, hand-off signalled (attention; 0 if this workgroup did not
- * finish a kv head) or Wo slice issued (Wo), poll passed (Wo), end. Workgroups
+ * finish a kv head) or Wo slice landed (Wo; the trace waits for it), poll passed (Wo), end. Workgroups
  * [0, *attention_workgroups) are attention, the rest Wo. */
 int yalm_attn_wo_trace(yalm_decoder d, unsigned long long *host, size_t count, int *workgroups,
                        int *attention_workgroups);

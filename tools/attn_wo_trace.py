@@ -47,7 +47,7 @@ def main():
     print(f"attention end    {q(att[:, 3])}")
     print(f"head signalled   {q(writers[:, 1])}  ({len(writers)} writers)")
     print(f"Wo start         {q(wo[:, 0])}")
-    print(f"Wo slice issued  {q(wo[:, 1])}")
+    print(f"Wo slice landed  {q(wo[:, 1])}")
     print(f"Wo poll passed   {q(wo[:, 2])}")
     print(f"Wo end           {q(wo[:, 3])}")
     dec.close()

@@ -57,7 +57,63 @@ struct AttnWoArgs {
 	unsigned *prev;     // the previous layer's counters (zeroed here)
 	unsigned *err;      // error bits (bounded spin gave up)
 	unsigned long long *trace; // [grid][4] s_memrealtime stamps (YALM_ATTN_WO_TRACE=1) or null
+	int win;            // Wo loads in flight per lane: 0 = all at once, 8 / 16 / 24 (YALM_ATTN_WO_WIN);
+	                    // -1 = no weight loads (timing only: isolates the attention chain, results wrong)
 };
+
+// Gather this lane's XS pieces of the attention output (EPL floats each, pieces
+// 256 * EPL floats apart) with 16-byte sc1 loads -- the hand-off's load form
+// (4- or 16-byte sc1 loads). 4-byte loads at a 32-byte lane stride made every
+// wave instruction request 16 lines for 256 useful bytes, 8 times over, from all
+// 256 Wo workgroups at once. hipcc does not track asm loads: one statement issues
+// them all and drains vmcnt (the weight slice has landed by then anyway).
+template <int EPL, int XS>
+__device__ __forceinline__ void awo_gather(float (&xs)[XS][EPL], const float *src) {
+	constexpr int NL = XS * EPL / 4; // 16-byte loads per lane: 2, 4 or 8
+	static_assert(NL == 2 || NL == 4 || NL == 8, "EPL * XS in {8, 16, 32}");
+	constexpr int LPP = EPL / 4;      // loads per piece
+	const float *a[8];
+#pragma unroll
+	for (int i = 0; i < NL; ++i)
+		a[i] = src + (size_t)(i / LPP) * ATTN_THREADS * EPL + (i % LPP) * 4;
+	u32x4_t v[8];
+	if constexpr (NL == 2) {
+		asm volatile("global_load_dwordx4 %0, %2, off sc1\n\t"
+		             "global_load_dwordx4 %1, %3, off sc1\n\t"
+		             "s_waitcnt vmcnt(0)"
+		             : "=&v"(v[0]), "=&v"(v[1])
+		             : "v"(a[0]), "v"(a[1])
+		             : "memory");
+	} else if constexpr (NL == 4) {
+		asm volatile("global_load_dwordx4 %0, %4, off sc1\n\t"
+		             "global_load_dwordx4 %1, %5, off sc1\n\t"
+		             "global_load_dwordx4 %2, %6, off sc1\n\t"
+		             "global_load_dwordx4 %3, %7, off sc1\n\t"
+		             "s_waitcnt vmcnt(0)"
+		             : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3])
+		             : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3])
+		             : "memory");
+	} else {
+		asm volatile("global_load_dwordx4 %0, %8, off sc1\n\t"
+		             "global_load_dwordx4 %1, %9, off sc1\n\t"
+		             "global_load_dwordx4 %2, %10, off sc1\n\t"
+		             "global_load_dwordx4 %3, %11, off sc1\n\t"
+		             "global_load_dwordx4 %4, %12, off sc1\n\t"
+		             "global_load_dwordx4 %5, %13, off sc1\n\t"
+		             "global_load_dwordx4 %6, %14, off sc1\n\t"
+		             "global_load_dwordx4 %7, %15, off sc1\n\t"
+		             "s_waitcnt vmcnt(0)"
+		             : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]),
+		               "=&v"(v[7])
+		             : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7])
+		             : "memory");
+	}
+#pragma unroll
+	for (int i = 0; i < NL * 4; ++i) {
+		const uint32_t w = v[i / 4][i % 4];
+		xs[i / EPL][i % EPL] = __uint_as_float(w);
+	}
+}
 
 template <class WT, int GT, int XS>
 __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__restrict__ q,
@@ -71,7 +127,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 	const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 	const int units = p.n_kv * p.S;
 	unsigned long long *tr = p.trace && tid == 0 ? p.trace + (size_t)b * 4 : nullptr;
-	if (tr) // [0] start, [1] hand-off signalled / Wo slice issued, [2] poll passed, [3] end
+	if (tr) // [0] start, [1] hand-off signalled / Wo slice landed, [2] poll passed, [3] end
 		tr[0] = __builtin_amdgcn_s_memrealtime(), tr[1] = tr[2] = tr[3] = 0;
 
 	if (b < units) { // ---- attention workgroup
@@ -101,51 +157,65 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 	const int lrow0 = min(row0, p.dim - AWO_RPW);
 	const char *wbase = p.wo + (size_t)lrow0 * p.q_dim * WT::BYTES;
 	u32x4_t wr[LPT];
+	// p.win > 0: at most win loads in flight per lane (a sliding window), so the
+	// slice does not fill the CU's memory queues ahead of the attention's loads
 #pragma unroll
-	for (int i = 0; i < LPT; ++i)
-		wr[i] = load_nt16(wbase + ((size_t)i * ATTN_THREADS + tid) * 16);
+	for (int i = 0; i < LPT; ++i) {
+		if (i >= 8) {
+			if (p.win == 8)
+				asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+			else if (p.win == 16 && i >= 16)
+				asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+			else if (p.win == 24 && i >= 24)
+				asm volatile("s_waitcnt vmcnt(23)" ::: "memory");
+		}
+		wr[i] = p.win >= 0 ? load_nt16(wbase + ((size_t)i * ATTN_THREADS + tid) * 16) : u32x4_t{0u, 0u, 0u, 0u};
+	}
 	if (j == 0 && tid < p.n_kv * AWO_REPL) // previous layer's counters: done, next used one token later
 		p.prev[tid * AWO_REPL_STRIDE] = 0u;
-	if (tr)
+	if (tr) { // tracing only: when the whole slice has landed
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 		tr[1] = __builtin_amdgcn_s_memrealtime();
+	}
 
-	// ---- per wave and input piece k: wait for the kv heads whose outputs the piece covers
-	// (its 64 * EPL columns span q heads e0 / D .. and kv groups / G), gather it with
-	// 4-byte sc1 loads, dot it into every resident row. The polling lane's wave loads
-	// only after the poll matched (MI355X_MICROARCH.md §visibility "Valid forms" row 2).
+	// ---- per wave: wait for every kv head its input pieces cover (piece k's 64 * EPL
+	// columns span q heads e0 / D .. and kv groups / G), then gather all pieces at
+	// once with 4-byte sc1 loads (one round trip) and dot them into every resident
+	// row. The polling lane's wave loads only after its polls matched
+	// (MI355X_MICROARCH.md §visibility "Valid forms" row 2).
 	const int G = p.n_heads / p.n_kv;
 	const int rep = (b % AWO_REPL) * AWO_REPL_STRIDE;
-	float a0[AWO_RPW], a1[AWO_RPW];
+	if (lane == 0) {
+		const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+		bool dead = false;
 #pragma unroll
-	for (int r = 0; r < AWO_RPW; ++r)
-		a0[r] = a1[r] = 0.0f;
-#pragma unroll
-	for (int k = 0; k < XS; ++k) {
-		const int e0 = (k * ATTN_THREADS + 64 * wave) * EPL;
-		const int g_lo = e0 / D / G, g_hi = (e0 + 64 * EPL - 1) / D / G;
-		if (lane == 0) {
-			for (int g = g_lo; g <= g_hi; ++g) {
+		for (int k = 0; k < XS; ++k) {
+			const int e0 = (k * ATTN_THREADS + 64 * wave) * EPL;
+			const int g_lo = e0 / D / G, g_hi = (e0 + 64 * EPL - 1) / D / G;
+			for (int g = g_lo; g <= g_hi && !dead; ++g) {
 				const unsigned *c = p.done + g * AWO_HEAD + rep;
-				const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 				while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
 					__builtin_amdgcn_s_sleep(1);
 					if (__builtin_amdgcn_s_memrealtime() - t0 > AWO_TIMEOUT) {
 						__hip_atomic_fetch_or(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+						dead = true;
 						break;
 					}
 				}
 			}
 		}
-		if (tr && k == XS - 1)
-			tr[2] = __builtin_amdgcn_s_memrealtime();
-		float xk[EPL];
-		const float *src = p.att + (size_t)(k * ATTN_THREADS + tid) * EPL;
+	}
+	if (tr)
+		tr[2] = __builtin_amdgcn_s_memrealtime();
+	float xs[XS][EPL];
+	awo_gather<EPL, XS>(xs, p.att + (size_t)tid * EPL);
+	float a0[AWO_RPW], a1[AWO_RPW];
 #pragma unroll
-		for (int e = 0; e < EPL; ++e)
-			xk[e] = eng_ld_sc1(src + e);
+	for (int r = 0; r < AWO_RPW; ++r) {
+		a0[r] = a1[r] = 0.0f;
 #pragma unroll
-		for (int r = 0; r < AWO_RPW; ++r)
-			eng_dot16<WT>(a0[r], a1[r], wr[r * XS + k], xk);
+		for (int k = 0; k < XS; ++k)
+			eng_dot16<WT>(a0[r], a1[r], wr[r * XS + k], xs[k]);
 	}
 	// ---- resident rows . slice; 4-row transposed wave reductions; fixed-order workgroup sum
 #pragma unroll

@@ -443,6 +443,8 @@ static int launch_attn_wo(yalm_decoder_s *d, const yalm_block_weights &w, int la
 	p.prev = d->awo_sync + (size_t)((layer + c.n_layers - 1) % c.n_layers) * slot;
 	p.err = d->awo_err;
 	p.trace = d->awo_trace;
+	static const int win = getenv("YALM_ATTN_WO_WIN") ? atoi(getenv("YALM_ATTN_WO_WIN")) : 0;
+	p.win = win;
 	const int G = c.n_heads / c.n_kv_heads;
 	if constexpr (WT::BYTES == 2 || WT::BYTES == 1) {
 		if (p.q_dim * WT::BYTES == 4096)
