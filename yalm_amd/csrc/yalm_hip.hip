@@ -398,7 +398,9 @@ static int attn_wo_init(yalm_decoder_s *d) {
 	const size_t slot = (size_t)c.n_kv_heads * AWO_HEAD; // per layer: one counter per kv head
 	TRY(dalloc(d, (void **)&d->awo_sync, sizeof(unsigned) * (c.n_layers * slot + AWO_REPL_STRIDE)));
 	d->awo_err = d->awo_sync + c.n_layers * slot;
-	d->awo_S = std::min(nchunks, 32); // key-chunk splits per kv head, as the standalone attention launch
+	// key-chunk splits per kv head, as the standalone attention launch (YALM_AWO_SPLITS: sweep knob)
+	const char *senv = getenv("YALM_AWO_SPLITS");
+	d->awo_S = std::min(nchunks, senv ? std::max(1, atoi(senv)) : 32);
 	d->awo_nb = c.n_kv_heads * d->awo_S + (c.dim + AWO_RPW - 1) / AWO_RPW;
 	const char *tenv = getenv("YALM_ATTN_WO_TRACE");
 	if (tenv && atoi(tenv) != 0)
