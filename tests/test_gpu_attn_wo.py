@@ -130,7 +130,7 @@ def test_attn_wo_long_context_split_attention():
 
 def test_attn_wo_replay_deterministic():
     """Bitwise-identical logits for the same token sequence on two decoders
-    (ordered merges and reductions; the hand-off counter is reset in-launch)."""
+    (ordered merges and reductions; epoch-tagged hand-off flags)."""
     cfg = BASE
     outs = []
     for _ in range(2):
@@ -147,3 +147,42 @@ def test_attn_wo_replay_deterministic():
             dec.close()
             dm.close()
     np.testing.assert_array_equal(outs[0], outs[1])
+
+
+def test_attn_wo_block_hook_any_layer_order():
+    """Block::block hook on the fused path (ADVICE r1): one layer run several
+    times in a row, a forward stopped part-way, then full forwards. The done
+    flags carry the launch epoch, so no order of layer launches can let a Wo
+    workgroup read a stale attention output; x and logits match the oracle."""
+    cfg = BASE
+    t, dm, dec = make(cfg, seed=12)
+    om = O.OracleModel(cfg, t)
+    try:
+        tok = 5
+        for pos in range(4):
+            lg = dec.forward(tok, pos)
+            lo = om.forward(tok, pos)
+            assert relerr(lg, lo) < 1e-3
+            tok = int(np.argmax(lo))
+        pos = 4
+        kv_sink, kv_pos, kv_len = M.kv_indices(cfg.max_seq_len, pos)
+        x0 = om.embed(tok)
+        dec.set_x(x0)
+        om.x[:] = x0
+        for rep in range(3):  # the same layer three times in a row
+            dec.block(1, pos, kv_sink, kv_pos, kv_len)
+            om.block(1, pos, kv_sink, kv_pos, kv_len)
+            e = relerr(dec.get_x(), om.x)
+            assert e < 1e-4, (rep, e)
+            dec.set_x(om.x)
+        dec.block(0, pos, kv_sink, kv_pos, kv_len)  # a forward stopped after layer 0
+        om.block(0, pos, kv_sink, kv_pos, kv_len)
+        assert relerr(dec.get_x(), om.x) < 1e-4
+        for pos in range(4, 12):  # full forwards after the out-of-order launches
+            lg = dec.forward(tok, pos)
+            lo = om.forward(tok, pos)
+            assert relerr(lg, lo) < 1e-3, (pos, relerr(lg, lo))
+            tok = int(np.argmax(lo))
+    finally:
+        dec.close()
+        dm.close()

@@ -8,26 +8,30 @@
 //   * ATTENTION workgroups [0, n_kv * S): attn_decode_body (attention.h) with
 //     write-through (sc1) head outputs; the workgroup that finishes kv head g
 //     (single-chunk writer or last arriver) drains its stores (vmcnt(0)), joins
-//     a workgroup barrier and adds 1 to every replica of kv head g's done
-//     counter (one wave instruction, 8 lanes). They issue no weight loads: a
+//     a workgroup barrier and stores the launch epoch (StepState::epoch) into
+//     every replica of kv head g's done flag (one wave instruction, 8 lanes, sc1
+//     stores). They issue no weight loads: a
 //     weight stream queued in front of the merge's loads (vmcnt is in order)
 //     would hold the whole hand-off behind it.
 //   * Wo workgroups [n_kv * S, grid): each owns AWO_RPW contiguous Wo rows and
 //     issues them as register loads at once, so the 33.5 MB stream runs while
 //     the attention works. Each WAVE then takes its input pieces in turn: its
-//     lane 0 polls the XCD replica of the done counter of every kv head the
-//     piece's columns cover (sc1 loads, bounded), the wave gathers the piece
-//     with 4-byte sc1 loads and dots it into every resident row
-//     (MI355X_MICROARCH.md §visibility, "Valid forms" row 2: counters kept in
-//     R = 8 replicas on lines of their own), so a wave works as soon as ITS
+//     lane 0 polls the XCD replica of the done flag of every kv head the
+//     piece's columns cover until it holds this launch's epoch (sc1 loads,
+//     bounded), the wave gathers the piece with 16-byte sc1 loads and dots it
+//     into every resident row (MI355X_MICROARCH.md §visibility, "Valid forms"
+//     row 1: one flag per producer, kept in R = 8 replicas on lines of their
+//     own), so a wave works as soon as ITS
 //     heads are done; then the rows are reduced across the workgroup in a
 //     fixed order and added to the residual (fused_matmul_add_residuals,
 //     infer.cu:270).
 // Workgroups dispatch in index order, so every attention workgroup is resident
 // before any Wo workgroup spins, and attention never waits on Wo: no deadlock
-// even when the grid is not co-resident. Counters: one slot of n_kv x 8
-// replicas per layer; layer l's launch zeroes layer l - 1's slot (finished, next used one
-// token later; n_layers >= 2), so there is no in-launch reset ticket (a
+// even when the grid is not co-resident. Flags: one slot of n_kv x 8 replicas
+// per layer, each holding the epoch of the last launch that finished that kv
+// head. The epoch grows by one per forward and per yalm_block call, so a flag
+// is never reset and any order of layer launches (one layer repeated, a forward
+// stopped part-way) stays correct; there is no in-launch reset ticket either (a
 // returning atomic from every workgroup costs ~6 us of serialised fan-in,
 // MI355X_MICROARCH.md row fanin). Every spin is bounded and reports in *err.
 //
@@ -53,12 +57,11 @@ struct AttnWoArgs {
 	float *att;         // attention output (q_dim), written sc1
 	const char *wo;     // Wo (dim, q_dim)
 	float *x;           // residual stream (dim)
-	unsigned *done;     // this layer's per-kv-head counters: [n_kv][AWO_REPL replicas, AWO_REPL_STRIDE words apart]
-	unsigned *prev;     // the previous layer's counters (zeroed here)
+	unsigned *done;     // this layer's per-kv-head done flags: [n_kv][AWO_REPL replicas, AWO_REPL_STRIDE words apart]
 	unsigned *err;      // error bits (bounded spin gave up)
 	unsigned long long *trace; // [grid][4] s_memrealtime stamps (YALM_ATTN_WO_TRACE=1) or null
 	int win;            // Wo loads in flight per lane: 0 = all at once, 8 / 16 / 24 (YALM_ATTN_WO_WIN);
-	                    // -1 = no weight loads (timing only: isolates the attention chain, results wrong)
+	                    // -1 = no weight loads (YALM_ABLATE bit 32, timing only: results wrong)
 };
 
 // Gather this lane's XS pieces of the attention output (EPL floats each, pieces
@@ -130,6 +133,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 	if (tr) // [0] start, [1] hand-off signalled / Wo slice landed, [2] poll passed, [3] end
 		tr[0] = __builtin_amdgcn_s_memrealtime(), tr[1] = tr[2] = tr[3] = 0;
 
+	const unsigned epoch = step->epoch; // this launch's tag (step_begin_kernel / set_step_full_kernel)
 	if (b < units) { // ---- attention workgroup
 		const bool wrote = attn_decode_body<D, GT, true>(true, b % p.n_kv, b / p.n_kv, p.S, q, kc, vc, step,
 		                                                 p.n_heads, p.n_kv, p.max_seq_len, p.nsplit, p.part,
@@ -138,8 +142,8 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 			asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // every storing wave drains its sc1 stores
 			__syncthreads();
 			if (tid < AWO_REPL) // kv head b % n_kv done: one wave instruction, one lane per replica
-				__hip_atomic_fetch_add(&p.done[(b % p.n_kv) * AWO_HEAD + tid * AWO_REPL_STRIDE], 1u,
-				                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+				__hip_atomic_store(&p.done[(b % p.n_kv) * AWO_HEAD + tid * AWO_REPL_STRIDE], epoch, __ATOMIC_RELAXED,
+				                   __HIP_MEMORY_SCOPE_AGENT);
 			if (tr)
 				tr[1] = __builtin_amdgcn_s_memrealtime();
 		}
@@ -171,8 +175,6 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 		}
 		wr[i] = p.win >= 0 ? load_nt16(wbase + ((size_t)i * ATTN_THREADS + tid) * 16) : u32x4_t{0u, 0u, 0u, 0u};
 	}
-	if (j == 0 && tid < p.n_kv * AWO_REPL) // previous layer's counters: done, next used one token later
-		p.prev[tid * AWO_REPL_STRIDE] = 0u;
 	if (tr) { // tracing only: when the whole slice has landed
 		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 		tr[1] = __builtin_amdgcn_s_memrealtime();
@@ -180,7 +182,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 
 	// ---- per wave: wait for every kv head its input pieces cover (piece k's 64 * EPL
 	// columns span q heads e0 / D .. and kv groups / G), then gather all pieces at
-	// once with 4-byte sc1 loads (one round trip) and dot them into every resident
+	// once with 16-byte sc1 loads (one round trip) and dot them into every resident
 	// row. The polling lane's wave loads only after its polls matched
 	// (MI355X_MICROARCH.md §visibility "Valid forms" row 2).
 	const int G = p.n_heads / p.n_kv;
@@ -194,7 +196,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 			const int g_lo = e0 / D / G, g_hi = (e0 + 64 * EPL - 1) / D / G;
 			for (int g = g_lo; g <= g_hi && !dead; ++g) {
 				const unsigned *c = p.done + g * AWO_HEAD + rep;
-				while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+				while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
 					__builtin_amdgcn_s_sleep(1);
 					if (__builtin_amdgcn_s_memrealtime() - t0 > AWO_TIMEOUT) {
 						__hip_atomic_fetch_or(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -87,7 +87,8 @@ struct yalm_decoder_s {
 	GemvCfg gemv[GK_N];
 	bool eager = false;     // YALM_EAGER=1: launch kernels directly (profilers that mis-handle graph replay)
 	bool graph_sync = false; // YALM_GRAPH_SYNC=1: synchronise after every replay
-	int ablate = 0;          // YALM_ABLATE bitmask: skip qkv|attn|wo|glu|w2 (1|2|4|8|16), timing only
+	int ablate = 0;          // YALM_ABLATE bitmask: skip qkv|attn|wo|glu|w2 (1|2|4|8|16), or (32) load no Wo
+	                         // weights in the fused attention + Wo launch; timing only, results wrong
 	std::string kname;
 	PrefillBufs pf;
 	// tensor parallelism (yalm_decoder_create_tp): c holds the LOCAL shard dims
@@ -126,7 +127,8 @@ struct yalm_decoder_s {
 	int awo_nb = 0;                  // grid: n_kv * awo_S attention + ceil(dim / AWO_RPW) Wo workgroups
 	int awo_S = 0;                   // key-chunk splits per kv head
 	unsigned long long *awo_trace = nullptr; // YALM_ATTN_WO_TRACE=1: [grid][4] stamps of the last launch
-	unsigned *awo_sync = nullptr;    // [n_layers][n_kv][AWO_HEAD] per-kv-head done counters, then the error word
+	int awo_win = 0;                 // Wo loads in flight per lane (YALM_ATTN_WO_WIN), -1 = none (ablation)
+	unsigned *awo_sync = nullptr;    // [n_layers][n_kv][AWO_HEAD] per-kv-head done flags (epochs), then the error word
 	unsigned *awo_err = nullptr;     // = awo_sync + n_layers * n_kv * AWO_HEAD
 };
 

@@ -23,7 +23,9 @@ struct StepState {
 	int kv_pos;  // infer.cu:1082
 	int kv_len;  // infer.cu:1083
 	int n_gen;   // number of greedy tokens produced so far (device loop)
-	int pad[2];
+	unsigned epoch; // launch generation: +1 per forward (step_begin_kernel) and per test-hook block
+	                // (set_step_full_kernel); in-launch hand-off flags carry it, so they never need a reset
+	int pad;
 };
 
 // Cross-lane exchange without the LDS crossbar: __shfl_xor lowers to

@@ -186,7 +186,8 @@ int engine_check(yalm_decoder_s *d) {
 	if (d->awo_err) { // the fused attention + Wo launch spins too (attn_wo.h)
 		unsigned e = 0;
 		HIPCHK(hipMemcpy(&e, d->awo_err, sizeof(e), hipMemcpyDeviceToHost));
-		if (e) {
+		if (e) { // reported once: cleared so that later calls report only their own failures
+			HIPCHK(hipMemset(d->awo_err, 0, sizeof(e)));
 			set_err("fused attention + Wo launch gave up waiting for the attention heads (error bits " +
 			        std::to_string(e) + "): grid not co-resident; YALM_ATTN_WO=0 selects separate launches");
 			return YALM_ERR_HIP;
@@ -197,6 +198,7 @@ int engine_check(yalm_decoder_s *d) {
 	unsigned e = 0;
 	HIPCHK(hipMemcpy(&e, d->eng_err, sizeof(e), hipMemcpyDeviceToHost));
 	if (e) {
+		HIPCHK(hipMemset(d->eng_err, 0, sizeof(e)));
 		set_err("persistent decode engine gave up waiting (error bits " + std::to_string(e) +
 		        "): grid not co-resident or a CU stalled; YALM_ENGINE=0 selects the launch path");
 		return YALM_ERR_HIP;

@@ -21,6 +21,7 @@ __global__ void set_step_full_kernel(StepState *st, int pos, int kv_sink, int kv
 	st->kv_sink = kv_sink;
 	st->kv_pos = kv_pos;
 	st->kv_len = kv_len;
+	st->epoch = st->epoch + 1u;
 }
 
 // First node of every forward graph: sliding-window indices (infer.cu:1081-
@@ -43,6 +44,7 @@ __global__ __launch_bounds__(256) void step_begin_kernel(StepState *st, const vo
 		st->kv_sink = kv_sink;
 		st->kv_pos = kv_sink + (pos - kv_sink) % (max_seq_len - kv_sink);
 		st->kv_len = pos >= max_seq_len ? max_seq_len : pos + 1;
+		st->epoch = st->epoch + 1u;
 	}
 }
 

@@ -372,8 +372,7 @@ static const void *attn_wo_pick(int dtype, int G, int XS) {
 	return XS == 1 ? attn_wo_fn_g<WF8, 1>(G) : attn_wo_fn_g<WF8, 2>(G);
 }
 
-// Single-GPU decoders with head_dim 128, G <= 8, fp16 / fp8 Wo rows of 4 or 8 KB and
-// at least 2 layers (layer l zeroes layer l - 1's hand-off counter).
+// Single-GPU decoders with head_dim 128, G <= 8 and fp16 / fp8 Wo rows of 4 or 8 KB.
 static int attn_wo_init(yalm_decoder_s *d) {
 	const yalm_config &c = d->c;
 	const char *env = getenv("YALM_ATTN_WO");
@@ -387,7 +386,7 @@ static int attn_wo_init(yalm_decoder_s *d) {
 	const int rb = c.n_heads * c.head_dim * (c.weight_dtype == YALM_F16 ? 2 : 1);
 	if (rb != 4096 && rb != 8192)
 		return YALM_OK;
-	if (c.dim < AWO_RPW || c.n_layers < 2 || c.n_kv_heads * AWO_REPL > ATTN_THREADS)
+	if (c.dim < AWO_RPW || c.n_kv_heads * AWO_REPL > ATTN_THREADS)
 		return YALM_OK;
 	int occ = 0; // the Wo workgroups spin, but only on attention workgroups dispatched before them
 	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, attn_wo_pick(c.weight_dtype, G, rb / 4096), ATTN_THREADS,
@@ -402,6 +401,14 @@ static int attn_wo_init(yalm_decoder_s *d) {
 	const char *senv = getenv("YALM_AWO_SPLITS");
 	d->awo_S = std::min(nchunks, senv ? std::max(1, atoi(senv)) : 32);
 	d->awo_nb = c.n_kv_heads * d->awo_S + (c.dim + AWO_RPW - 1) / AWO_RPW;
+	// Wo loads in flight per lane (tuning knob): 0 = the whole slice at once, or 8 / 16 / 24
+	const char *wenv = getenv("YALM_ATTN_WO_WIN");
+	const int win = wenv ? atoi(wenv) : 0;
+	if (win != 0 && win != 8 && win != 16 && win != 24) {
+		set_err("YALM_ATTN_WO_WIN must be 0, 8, 16 or 24");
+		return YALM_ERR_ARG;
+	}
+	d->awo_win = d->ablate & 32 ? -1 : win; // ablation bit 32: no Wo weight loads (timing only)
 	const char *tenv = getenv("YALM_ATTN_WO_TRACE");
 	if (tenv && atoi(tenv) != 0)
 		TRY(dalloc(d, (void **)&d->awo_trace, sizeof(unsigned long long) * 4 * d->awo_nb));
@@ -442,11 +449,9 @@ static int launch_attn_wo(yalm_decoder_s *d, const yalm_block_weights &w, int la
 	p.x = d->x;
 	const size_t slot = (size_t)c.n_kv_heads * AWO_HEAD;
 	p.done = d->awo_sync + (size_t)layer * slot;
-	p.prev = d->awo_sync + (size_t)((layer + c.n_layers - 1) % c.n_layers) * slot;
 	p.err = d->awo_err;
 	p.trace = d->awo_trace;
-	static const int win = getenv("YALM_ATTN_WO_WIN") ? atoi(getenv("YALM_ATTN_WO_WIN")) : 0;
-	p.win = win;
+	p.win = d->awo_win;
 	const int G = c.n_heads / c.n_kv_heads;
 	if constexpr (WT::BYTES == 2 || WT::BYTES == 1) {
 		if (p.q_dim * WT::BYTES == 4096)
