@@ -43,25 +43,25 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(kernel_prefix, dtype):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3
-    --pmc FETCH_SIZE pass (profiles/*_pmc_fetch_size_glu.csv): median
-    FETCH_SIZE (KB) x 1024 x 2 — gfx950 counts half the bytes of 16 B/lane
-    streaming reads (MI355X_MICROARCH.md §HBM). None if no matching profile."""
+def pmc_traffic(kernel_match, dtype):
+    """HBM bytes per launch of the dominant kernel from the newest committed
+    rocprofv3 --pmc FETCH_SIZE pass that profiled it (profiles/*_pmc_fetch_size*.csv):
+    median FETCH_SIZE (KB) x 1024 x 2 -- gfx950 counts half the bytes of 16 B/lane
+    streaming reads (MI355X_MICROARCH.md §HBM). `kernel_match`: substrings that
+    must all appear in the kernel name. None if no matching profile."""
     import csv
     import glob
     import statistics
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_fetch_size_glu.csv")))
-    if not files or dtype != "fp16":
+    if dtype != "fp16":
         return None, None
-    rows = list(csv.DictReader(open(files[-1])))
-    vals = [float(r["Counter_Value"]) for r in rows
-            if r["Counter_Name"] == "FETCH_SIZE" and kernel_prefix.split("<")[0] in r["Kernel_Name"]
-            and "PGlu" in r["Kernel_Name"]]
-    if not vals:
-        return None, None
-    return int(statistics.median(vals) * 1024 * 2), os.path.relpath(files[-1], ROOT)
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_fetch_size*.csv")), reverse=True):
+        rows = list(csv.DictReader(open(f)))
+        vals = [float(r["Counter_Value"]) for r in rows
+                if r["Counter_Name"] == "FETCH_SIZE" and all(k in r["Kernel_Name"] for k in kernel_match)]
+        if vals:
+            return int(statistics.median(vals) * 1024 * 2), os.path.relpath(f, ROOT)
+    return None, None
 
 
 def cpu_baseline(cfg, budget_s):
@@ -188,15 +188,24 @@ def main():
     _, pos1 = dec.device_step()
     assert pos1 - pos0 == args.steps, (pos0, pos1)
 
-    # ---- roofline of the dominant kernel: W1/W3 GEMV + SiLU-GLU (52.9% of bytes)
-    KID = 3
-    avg_ms = dec.time_kernel(KID, args.kernel_iters)
+    # ---- roofline of the dominant kernel: the fused feed-forward launch (rmsnorm +
+    # W1/W3 + GLU + W2 + residual, 79.3% of the bytes) when the decoder runs it, else
+    # the W1/W3 GEMV + SiLU-GLU (52.9% of the bytes)
     wb = M.DTYPE_BYTES[cfg.weight_dtype]
     hid_local = cfg.hidden_dim // (world if args.tp else 1)
-    glu_bytes = 2 * hid_local * cfg.dim * wb + 2 * cfg.dim * 4 + hid_local * 4
-    achieved = glu_bytes / (avg_ms * 1e-3) / 1e9
+    if dec.ffn:
+        KID = 7
+        # W1, W3, W2 + rms_ffn + x read + x rows written + hb written once
+        kern_bytes = 3 * hid_local * cfg.dim * wb + 3 * cfg.dim * 4 + hid_local * 4
+        match = ("ffn_kernel<WF16",)
+    else:
+        KID = 3
+        kern_bytes = 2 * hid_local * cfg.dim * wb + 2 * cfg.dim * 4 + hid_local * 4
+        match = ("gemv_rb_kernel<WF16", "PGlu")
+    avg_ms = dec.time_kernel(KID, args.kernel_iters)
+    achieved = kern_bytes / (avg_ms * 1e-3) / 1e9
     kname = dec.kernel_name(KID)
-    traffic, traffic_src = pmc_traffic(kname, args.dtype)
+    traffic, traffic_src = pmc_traffic(match, args.dtype)
 
     toks = args.steps * (1 if args.tp else world)
     value = toks / elapsed
@@ -243,7 +252,7 @@ def main():
             "bound": "hbm",
             "kernel": kname,
             "avg_launch_us": round(avg_ms * 1e3, 3),
-            "algorithmic_bytes_per_launch": int(glu_bytes),
+            "algorithmic_bytes_per_launch": int(kern_bytes),
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

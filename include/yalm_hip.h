@@ -136,7 +136,9 @@ int yalm_get_logits(yalm_decoder d, float *host);
  * the decoder's stream `iters` times between HIP events. kernel_id: 0 = QKV
  * GEMV, 1 = attention, 2 = Wo GEMV, 3 = W1/W3 GEMV+GLU, 4 = W2 GEMV,
  * 5 = logits GEMV, 6 = the whole-token engine launch (greedy mode; advances
- * the decoder's device step). Used by bench.py for the roofline of the dominant kernel. */
+ * the decoder's device step), 7 = the fused feed-forward launch (rmsnorm + W1/W3
+ * + GLU + W2 + residual, yalm_decoder_ffn). Used by bench.py for the roofline
+ * of the dominant kernel. */
 int yalm_time_kernel(yalm_decoder d, int kernel_id, int iters, float *avg_ms);
 /* Override the GEMV launch geometry of one weight-streaming kernel kind
  * (0 = QKV, 1 = Wo, 2 = W1/W3, 3 = W2, 4 = logits): workgroup size
@@ -167,6 +169,21 @@ int yalm_decoder_attn_wo(yalm_decoder d);
  * [0, *attention_workgroups) are attention, the rest Wo. */
 int yalm_attn_wo_trace(yalm_decoder d, unsigned long long *host, size_t count, int *workgroups,
                        int *attention_workgroups);
+/* 1 if this decoder's launch path runs the whole feed-forward half of a block
+ * (rmsnorm, W1/W3 + SiLU/GELU-GLU, W2 + residual; infer.cu:598-620 + 270-288,
+ * which the reference launches as three kernels) as ONE launch (ffn.h: the W2
+ * weight stream is in flight while the last GLU rows finish; the hb hand-off is
+ * an in-launch seam over all workgroups, one per CU): single GPU, fp16 / fp8
+ * weights, dim and hidden_dim multiples of 512 (fp16) / 1024 (fp8) elements,
+ * and YALM_FFN=1 at creation (opt-in: slower than the separate launches on
+ * MI355X). 0 = separate GLU and W2 launches. */
+int yalm_decoder_ffn(yalm_decoder d);
+/* Timeline of the most recent fused feed-forward launch (decoder created with
+ * YALM_FFN_TRACE=1): 8 words per workgroup at [w * 8 + k]: s_memrealtime
+ * (100 MHz) at start, GLU partials done, hb published, every workgroup's flag
+ * seen, hb gathered into LDS, end; then (GLU items | W2 items << 32) of wave 0.
+ * *workgroups = grid size. Profiling hook. */
+int yalm_ffn_trace(yalm_decoder d, unsigned long long *host, size_t count, int *workgroups);
 /* Timeline of the engine's most recent launch (decoder created with
  * YALM_ENGINE_TRACE=1): for workgroup w and phase p (5 per layer: QKV,
  * attention, Wo, W1/W3, W2; then logits; the last index 5 L + 1 holds per-CU

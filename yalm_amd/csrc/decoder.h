@@ -130,6 +130,15 @@ struct yalm_decoder_s {
 	int awo_win = 0;                 // Wo loads in flight per lane (YALM_ATTN_WO_WIN), -1 = none (ablation)
 	unsigned *awo_sync = nullptr;    // [n_layers][n_kv][AWO_HEAD] per-kv-head done flags (epochs), then the error word
 	unsigned *awo_err = nullptr;     // = awo_sync + n_layers * n_kv * AWO_HEAD
+	// launch path: rmsnorm + GLU + W2 + residual as one launch (ffn.h) when
+	// supported; YALM_FFN=0 selects the separate GLU and W2 kernels
+	bool ffn = false;
+	int ffn_nb = 0;                  // workgroups = CUs (all co-resident)
+	int ffn_P = 8;                   // extra W2 loads in flight per wave across the seam (YALM_FFN_P)
+	size_t ffn_lds = 0;              // dynamic LDS bytes
+	unsigned *ffn_flags = nullptr;   // [n_layers][ffn_nb] per-workgroup epochs, then the error word
+	unsigned *ffn_err = nullptr;
+	unsigned long long *ffn_trace = nullptr; // YALM_FFN_TRACE=1: [ffn_nb][8] stamps of the last launch
 };
 
 // ------------------------------------------------------------------ shared helpers

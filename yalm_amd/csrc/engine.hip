@@ -193,6 +193,16 @@ int engine_check(yalm_decoder_s *d) {
 			return YALM_ERR_HIP;
 		}
 	}
+	if (d->ffn_err) { // and the fused feed-forward launch (ffn.h)
+		unsigned e = 0;
+		HIPCHK(hipMemcpy(&e, d->ffn_err, sizeof(e), hipMemcpyDeviceToHost));
+		if (e) {
+			HIPCHK(hipMemset(d->ffn_err, 0, sizeof(e)));
+			set_err("fused feed-forward launch gave up waiting for the hb of every workgroup (error bits " +
+			        std::to_string(e) + "): grid not co-resident; YALM_FFN=0 selects separate launches");
+			return YALM_ERR_HIP;
+		}
+	}
 	if (!d->engine)
 		return YALM_OK;
 	unsigned e = 0;

@@ -20,6 +20,7 @@
 #include "attn_wo.h"
 #include "decoder.h"
 #include "device_common.h"
+#include "ffn.h"
 #include "gemv.h"
 #include "misc_kernels.h"
 
@@ -463,6 +464,97 @@ static int launch_attn_wo(yalm_decoder_s *d, const yalm_block_weights &w, int la
 	return YALM_OK;
 }
 
+// ---- rmsnorm + GLU + W2 + residual in one launch (ffn.h)
+#define FFN_U 4
+template <class WT, int ACT>
+static const void *ffn_fn(int P) {
+	switch (P) {
+	case 0:
+		return (const void *)ffn_kernel<WT, ACT, FFN_U, 0>;
+	case 4:
+		return (const void *)ffn_kernel<WT, ACT, FFN_U, 4>;
+	case 12:
+		return (const void *)ffn_kernel<WT, ACT, FFN_U, 12>;
+	default:
+		return (const void *)ffn_kernel<WT, ACT, FFN_U, 8>;
+	}
+}
+static const void *ffn_pick(int dtype, int act, int P) {
+	if (dtype == YALM_F16)
+		return act == YALM_SILU ? ffn_fn<WF16, 1>(P) : ffn_fn<WF16, 0>(P);
+	return act == YALM_SILU ? ffn_fn<WF8, 1>(P) : ffn_fn<WF8, 0>(P);
+}
+
+// Single-GPU decoders with fp16 / fp8 weights and dim, hidden_dim multiples of
+// one 1-KB chunk per wave instruction (512 fp16 / 1024 fp8 elements).
+static int ffn_init(yalm_decoder_s *d) {
+	const yalm_config &c = d->c;
+	// opt-in (YALM_FFN=1): measured slower than the separate launches on MI355X
+	// (Mistral-7B fp16: 59.5-61 us per launch against 38.7 + 20.8 us):
+	// the in-launch seam (slowest workgroup + hb publish + flag propagation + gather,
+	// ~6 us) costs more than the kernel boundary it replaces
+	const char *env = getenv("YALM_FFN");
+	if (!env || atoi(env) == 0)
+		return YALM_OK;
+	if (d->comm || d->ipc || d->tp_size > 1 || d->engine)
+		return YALM_OK;
+	if (c.weight_dtype != YALM_F16 && c.weight_dtype != YALM_F8E5M2)
+		return YALM_OK;
+	const int CH = c.weight_dtype == YALM_F16 ? 512 : 1024;
+	if (c.dim % CH != 0 || c.hidden_dim % CH != 0)
+		return YALM_OK;
+	const char *penv = getenv("YALM_FFN_P");
+	const int P = penv ? atoi(penv) : 8;
+	if (P != 0 && P != 4 && P != 8 && P != 12) {
+		set_err("YALM_FFN_P must be 0, 4, 8 or 12");
+		return YALM_ERR_ARG;
+	}
+	const int nb = device_cu_count();
+	const size_t lds = ffn_lds_floats(c.dim, c.hidden_dim, nb) * sizeof(float);
+	if (lds > 160 * 1024)
+		return YALM_OK;
+	const void *fn = ffn_pick(c.weight_dtype, c.act, P);
+	if (lds > 65536)
+		HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+	// the seam waits on every workgroup: the whole grid (one per CU) must be resident
+	int occ = 0;
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, FFN_THREADS, lds) != hipSuccess || occ < 1)
+		return YALM_OK;
+	d->ffn_nb = nb;
+	d->ffn_P = P;
+	d->ffn_lds = lds;
+	TRY(dalloc(d, (void **)&d->ffn_flags, sizeof(unsigned) * ((size_t)c.n_layers * nb + 64)));
+	d->ffn_err = d->ffn_flags + (size_t)c.n_layers * nb;
+	const char *tenv = getenv("YALM_FFN_TRACE");
+	if (tenv && atoi(tenv) != 0)
+		TRY(dalloc(d, (void **)&d->ffn_trace, sizeof(unsigned long long) * FFN_TRACE_WORDS * nb));
+	d->ffn = true;
+	return YALM_OK;
+}
+
+template <class WT>
+static int launch_ffn(yalm_decoder_s *d, const yalm_block_weights &w, int layer) {
+	const yalm_config &c = d->c;
+	FfnArgs p;
+	p.w1 = (const char *)w.w1;
+	p.w3 = (const char *)w.w3;
+	p.w2 = (const char *)w.w2;
+	p.normw = w.rms_ffn;
+	p.eps = c.norm_eps;
+	p.x = d->x;
+	p.hb = d->hb;
+	p.flags = d->ffn_flags + (size_t)layer * d->ffn_nb;
+	p.err = d->ffn_err;
+	p.step = d->step;
+	p.dim = c.dim;
+	p.hidden = c.hidden_dim;
+	p.trace = d->ffn_trace;
+	const void *fn = ffn_pick(c.weight_dtype, c.act, d->ffn_P);
+	void *args[] = {&p};
+	HIPCHK(hipLaunchKernel(fn, dim3(d->ffn_nb), dim3(FFN_THREADS), args, d->ffn_lds, d->stream));
+	return YALM_OK;
+}
+
 static const unsigned *ipc_seq(const yalm_decoder_s *d) {
 	return (const unsigned *)(d->ipc_own + 2 * (size_t)d->ipc_S) + 64;
 }
@@ -555,6 +647,11 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 			                c.max_seq_len, d->part, d->attn_counters, nullptr, d->xb2, st));
 		if (!(ab & 4))
 			TRY(enqueue_residual_gemv<WT>(d, w.wo, q_dim, d->xb2, GK_WO));
+	}
+	if (d->ffn && WT::BYTES <= 2) {
+		if (!(ab & 24))
+			TRY(launch_ffn<WT>(d, w, l));
+		return YALM_OK;
 	}
 	if (ab & 8) {
 	} else if (c.act == YALM_SILU) {
@@ -827,7 +924,7 @@ static int create_decoder(const yalm_config *config, const yalm_model_weights *w
 		set_err("hipHostMalloc failed");
 		return fail(YALM_ERR_HIP);
 	}
-	if ((r = engine_init(d)) || (r = attn_wo_init(d)))
+	if ((r = engine_init(d)) || (r = attn_wo_init(d)) || (r = ffn_init(d)))
 		return fail(r);
 	if (hipDeviceSynchronize() != hipSuccess) {
 		set_err("hipDeviceSynchronize failed after decoder allocation");
@@ -1115,6 +1212,10 @@ static int enqueue_one_t(yalm_decoder_s *d, int kernel_id, int l) {
 		                   c.max_seq_len, d->part, d->attn_counters, nullptr, d->xb2, d->stream);
 	case 5:
 		return enqueue_logits_t<WT>(d);
+	case 7:
+		if constexpr (WT::BYTES <= 2)
+			return launch_ffn<WT>(d, w, l);
+		break;
 	}
 	set_err("bad kernel_id");
 	return YALM_ERR_ARG;
@@ -1126,6 +1227,21 @@ extern "C" int yalm_decoder_engine(yalm_decoder d) {
 
 extern "C" int yalm_decoder_attn_wo(yalm_decoder d) {
 	return d && d->attn_wo ? 1 : 0;
+}
+
+extern "C" int yalm_decoder_ffn(yalm_decoder d) {
+	return d && d->ffn ? 1 : 0;
+}
+
+extern "C" int yalm_ffn_trace(yalm_decoder d, unsigned long long *host, size_t count, int *workgroups) {
+	ARGCHK(d && host, "null argument");
+	ARGCHK(d->ffn && d->ffn_trace, "no ffn trace (create the decoder with YALM_FFN_TRACE=1)");
+	HIPCHK(hipStreamSynchronize(d->stream));
+	const size_t total = (size_t)FFN_TRACE_WORDS * d->ffn_nb;
+	HIPCHK(hipMemcpy(host, d->ffn_trace, sizeof(unsigned long long) * std::min(count, total), hipMemcpyDeviceToHost));
+	if (workgroups)
+		*workgroups = d->ffn_nb;
+	return YALM_OK;
 }
 
 extern "C" int yalm_attn_wo_trace(yalm_decoder d, unsigned long long *host, size_t count, int *workgroups,
@@ -1143,8 +1259,9 @@ extern "C" int yalm_attn_wo_trace(yalm_decoder d, unsigned long long *host, size
 }
 
 extern "C" int yalm_time_kernel(yalm_decoder d, int kernel_id, int iters, float *avg_ms) {
-	ARGCHK(d && avg_ms && iters > 0 && kernel_id >= 0 && kernel_id <= 6, "bad argument");
+	ARGCHK(d && avg_ms && iters > 0 && kernel_id >= 0 && kernel_id <= 7, "bad argument");
 	ARGCHK(kernel_id != 6 || d->engine, "kernel 6 (engine) needs a decoder running the persistent engine");
+	ARGCHK(kernel_id != 7 || d->ffn, "kernel 7 (fused feed-forward) needs a decoder with yalm_decoder_ffn");
 	hipEvent_t e0, e1;
 	HIPCHK(hipEventCreate(&e0));
 	HIPCHK(hipEventCreate(&e1));
@@ -1224,6 +1341,9 @@ extern "C" const char *yalm_kernel_name(yalm_decoder d, int kernel_id) {
 		break;
 	case 5:
 		s = gk + wt + ", PStore<";
+		break;
+	case 7:
+		s = std::string("ffn_kernel<") + wt + ", ";
 		break;
 	default:
 		s = "";
