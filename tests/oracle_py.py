@@ -168,11 +168,13 @@ class OracleModel:
         wcls = self.t.get("model.output.weight", emb)
         self.om = OModel(self.oc, P(emb), P(self.t["model.norm.weight"]), P(wcls), self.blocks)
         # xb2 holds the attention output (q_dim floats) and later the W2 output
-        # (dim): the reference sizes it dim (its models have q_dim == dim)
+        # (dim): the reference sizes it dim (its models have q_dim == dim); hb holds
+        # the Wo output (dim floats, infer.cpp:332) before the GLU (hidden_dim): the
+        # reference sizes it hidden_dim (its models have hidden_dim > dim)
         self.buf = {
             "x": np.zeros(c.dim, np.float32), "xb": np.zeros(c.dim, np.float32),
             "xb2": np.zeros(max(c.dim, c.q_dim), np.float32),
-            "hb": np.zeros(c.hidden_dim, np.float32), "hb2": np.zeros(c.hidden_dim, np.float32),
+            "hb": np.zeros(max(c.hidden_dim, c.dim), np.float32), "hb2": np.zeros(c.hidden_dim, np.float32),
             "q": np.zeros(c.q_dim, np.float32), "k": np.zeros(c.kv_dim, np.float32),
             "v": np.zeros(c.kv_dim, np.float32), "att": np.zeros(c.n_heads * c.max_seq_len, np.float32),
             "logits": np.zeros(c.vocab_size, np.float32),

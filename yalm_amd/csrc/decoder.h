@@ -47,6 +47,13 @@ enum { GK_QKV = 0, GK_WO = 1, GK_GLU = 2, GK_W2 = 3, GK_CLS = 4, GK_N = 5 };
 
 int device_cu_count();
 
+// Work-stealing row-block GEMV (gemv_dyn.h, dyn.hip): launches policy P's GEMV
+// with a static prefix + dequeued tail; DYN_FALLBACK when the shape does not fit
+// (the caller then launches gemv_rb_kernel). ctr: DYN_SHARDS counters, zero at rest.
+#define DYN_FALLBACK (-100)
+template <class WT, class P, bool NORM>
+int launch_dyn(const P &p, const float *x, const float *normw, float eps, unsigned *ctr, int frac_pct, hipStream_t st);
+
 // Batched-prefill scratch (prefill.hip), allocated on first use for
 // max_seq_len rows.
 struct PrefillBufs {
@@ -139,6 +146,11 @@ struct yalm_decoder_s {
 	unsigned *ffn_flags = nullptr;   // [n_layers][ffn_nb] per-workgroup epochs, then the error word
 	unsigned *ffn_err = nullptr;
 	unsigned long long *ffn_trace = nullptr; // YALM_FFN_TRACE=1: [ffn_nb][8] stamps of the last launch
+	// work-stealing tail for the weight-streaming GEMVs (gemv_dyn.h), opt-in YALM_DYN=1
+	// (slower than the static row-block kernel as measured); YALM_DYN_FRAC = percent pooled
+	bool dyn = false;
+	int dyn_frac = 10;
+	unsigned *dyn_ctr = nullptr;     // DYN_SHARDS counters, 32 words apart (self-resetting per launch)
 };
 
 // ------------------------------------------------------------------ shared helpers

@@ -22,6 +22,7 @@
 #include "device_common.h"
 #include "ffn.h"
 #include "gemv.h"
+#include "gemv_dyn.h"
 #include "misc_kernels.h"
 
 // ------------------------------------------------------------------ errors
@@ -291,6 +292,21 @@ static int launch_gemv(const P &p, const float *x, const float *normw, float eps
 		                : launch_stream<WT, P, NORM, 512, 8>(p, x, normw, eps, c.gpw, lds, st);
 	return c.U == 4 ? launch_stream<WT, P, NORM, 256, 4>(p, x, normw, eps, c.gpw, lds, st)
 	                : launch_stream<WT, P, NORM, 256, 8>(p, x, normw, eps, c.gpw, lds, st);
+}
+
+// The decoder's weight-streaming GEMVs: the work-stealing row-block kernel
+// (gemv_dyn.h) when enabled and the shape fits, else gemv_rb_kernel (or the
+// geometry set through yalm_set_gemv_config).
+template <class WT, class P, bool NORM>
+static int launch_gemv_d(yalm_decoder_s *d, const P &p, const float *x, const float *normw, float eps, int kind) {
+	if constexpr (WT::BYTES <= 2) {
+		if (d->dyn && !d->gemv[kind].threads) {
+			const int r = launch_dyn<WT, P, NORM>(p, x, normw, eps, d->dyn_ctr, d->dyn_frac, d->stream);
+			if (r != DYN_FALLBACK)
+				return r;
+		}
+	}
+	return launch_gemv<WT, P, NORM>(p, x, normw, eps, kind, d->gemv[kind], d->stream);
 }
 
 static bool attn_supported(int head_dim, int G) {
@@ -589,7 +605,7 @@ static int enqueue_residual_gemv(yalm_decoder_s *d, const void *W, int n, const 
 		p.n = n;
 		p.out = d->x;
 		p.n_groups = c.dim;
-		return launch_gemv<WT, PResidual<WT, 1>, false>(p, v, nullptr, 0.f, kind, d->gemv[kind], st);
+		return launch_gemv_d<WT, PResidual<WT, 1>, false>(d, p, v, nullptr, 0.f, kind);
 	}
 	if (d->tp_rank == 0) {
 		PAddTo<WT, 1> p;
@@ -637,7 +653,7 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 		p.q_out = d->q;
 		p.kcache = w.key_cache;
 		p.vcache = w.value_cache;
-		TRY((launch_gemv<WT, PQKV<WT>, true>(p, d->x, w.rms_att, c.norm_eps, GK_QKV, d->gemv[GK_QKV], st)));
+		TRY((launch_gemv_d<WT, PQKV<WT>, true>(d, p, d->x, w.rms_att, c.norm_eps, GK_QKV)));
 	}
 	if (d->attn_wo && WT::BYTES <= 2 && !(ab & 6)) {
 		TRY(launch_attn_wo<WT>(d, w, l));
@@ -661,7 +677,7 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 		p.n = c.dim;
 		p.out = d->hb;
 		p.n_groups = c.hidden_dim;
-		TRY((launch_gemv<WT, PGlu<WT, 1>, true>(p, d->x, w.rms_ffn, c.norm_eps, GK_GLU, d->gemv[GK_GLU], st)));
+		TRY((launch_gemv_d<WT, PGlu<WT, 1>, true>(d, p, d->x, w.rms_ffn, c.norm_eps, GK_GLU)));
 	} else {
 		PGlu<WT, 0> p;
 		p.w1 = (const char *)w.w1;
@@ -669,7 +685,7 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 		p.n = c.dim;
 		p.out = d->hb;
 		p.n_groups = c.hidden_dim;
-		TRY((launch_gemv<WT, PGlu<WT, 0>, true>(p, d->x, w.rms_ffn, c.norm_eps, GK_GLU, d->gemv[GK_GLU], st)));
+		TRY((launch_gemv_d<WT, PGlu<WT, 0>, true>(d, p, d->x, w.rms_ffn, c.norm_eps, GK_GLU)));
 	}
 	if (!(ab & 16))
 		TRY(enqueue_residual_gemv<WT>(d, w.w2, c.hidden_dim, d->hb, GK_W2));
@@ -698,14 +714,14 @@ static int enqueue_logits_t(yalm_decoder_s *d) {
 		p.n = c.dim;
 		p.out = d->logits_local;
 		p.n_groups = c.vocab_size / 2;
-		return launch_gemv<WT, PStore<WT, 2>, true>(p, d->x, d->rms_final, c.norm_eps, GK_CLS, d->gemv[GK_CLS], d->stream);
+		return launch_gemv_d<WT, PStore<WT, 2>, true>(d, p, d->x, d->rms_final, c.norm_eps, GK_CLS);
 	}
 	PStore<WT, 1> p;
 	p.W = (const char *)d->wcls;
 	p.n = c.dim;
 	p.out = d->logits_local;
 	p.n_groups = c.vocab_size;
-	return launch_gemv<WT, PStore<WT, 1>, true>(p, d->x, d->rms_final, c.norm_eps, GK_CLS, d->gemv[GK_CLS], d->stream);
+	return launch_gemv_d<WT, PStore<WT, 1>, true>(d, p, d->x, d->rms_final, c.norm_eps, GK_CLS);
 }
 
 template <class WT>
@@ -926,6 +942,19 @@ static int create_decoder(const yalm_config *config, const yalm_model_weights *w
 	}
 	if ((r = engine_init(d)) || (r = attn_wo_init(d)) || (r = ffn_init(d)))
 		return fail(r);
+	{ // work-stealing GEMV tail (gemv_dyn.h): single-GPU launch path, fp16 / fp8 weights.
+	  // Opt-in (YALM_DYN=1): measured slower on MI355X (Mistral-7B fp16: QKV 15.1 vs 12.0 us,
+	  // W1|W3 44.4 vs 39.6, W2 23.7 vs 20.8; static prefix alone 1-3 us slower)
+		const char *e = getenv("YALM_DYN");
+		const char *fr = getenv("YALM_DYN_FRAC");
+		d->dyn_frac = fr ? std::max(0, std::min(50, atoi(fr))) : 10;
+		if (e && atoi(e) != 0 && !d->engine && !d->comm && !d->ipc && tp_size == 1 &&
+		    (c.weight_dtype == YALM_F16 || c.weight_dtype == YALM_F8E5M2)) {
+			if ((r = dalloc(d, (void **)&d->dyn_ctr, sizeof(unsigned) * DYN_SHARDS * DYN_STRIDE)))
+				return fail(r);
+			d->dyn = true;
+		}
+	}
 	if (hipDeviceSynchronize() != hipSuccess) {
 		set_err("hipDeviceSynchronize failed after decoder allocation");
 		return fail(YALM_ERR_HIP);
@@ -1188,7 +1217,7 @@ static int enqueue_one_t(yalm_decoder_s *d, int kernel_id, int l) {
 			p.q_out = d->q;
 			p.kcache = w.key_cache;
 			p.vcache = w.value_cache;
-			return launch_gemv<WT, PQKV<WT>, true>(p, d->x, w.rms_att, c.norm_eps, GK_QKV, d->gemv[GK_QKV], d->stream);
+			return launch_gemv_d<WT, PQKV<WT>, true>(d, p, d->x, w.rms_att, c.norm_eps, GK_QKV);
 		}
 		if (kernel_id == 2 || kernel_id == 4) {
 			PResidual<WT, 1> p;
@@ -1196,8 +1225,8 @@ static int enqueue_one_t(yalm_decoder_s *d, int kernel_id, int l) {
 			p.n = kernel_id == 2 ? q_dim : c.hidden_dim;
 			p.out = d->x;
 			p.n_groups = c.dim;
-			return launch_gemv<WT, PResidual<WT, 1>, false>(p, kernel_id == 2 ? d->xb2 : d->hb, nullptr, 0.f, kernel_id == 2 ? GK_WO : GK_W2, d->gemv[kernel_id == 2 ? GK_WO : GK_W2],
-			                                               d->stream);
+			return launch_gemv_d<WT, PResidual<WT, 1>, false>(d, p, kernel_id == 2 ? d->xb2 : d->hb, nullptr, 0.f,
+			                                                  kernel_id == 2 ? GK_WO : GK_W2);
 		}
 		PGlu<WT, 1> p;
 		p.w1 = (const char *)w.w1;
@@ -1205,7 +1234,7 @@ static int enqueue_one_t(yalm_decoder_s *d, int kernel_id, int l) {
 		p.n = c.dim;
 		p.out = d->hb;
 		p.n_groups = c.hidden_dim;
-		return launch_gemv<WT, PGlu<WT, 1>, true>(p, d->x, w.rms_ffn, c.norm_eps, GK_GLU, d->gemv[GK_GLU], d->stream);
+		return launch_gemv_d<WT, PGlu<WT, 1>, true>(d, p, d->x, w.rms_ffn, c.norm_eps, GK_GLU);
 	}
 	case 1:
 		return launch_attn(c.head_dim, c.n_heads, c.n_kv_heads, d->q, w.key_cache, w.value_cache, d->step,
@@ -1321,7 +1350,7 @@ extern "C" const char *yalm_kernel_name(yalm_decoder d, int kernel_id) {
 	const char *wt = d->c.weight_dtype == YALM_F32 ? "WF32" : d->c.weight_dtype == YALM_F16 ? "WF16" : "WF8";
 	std::string s;
 	static const bool legacy = getenv("YALM_GEMV_LEGACY") && atoi(getenv("YALM_GEMV_LEGACY")) != 0;
-	const std::string gk = legacy ? "gemv_stream_kernel<" : "gemv_rb_kernel<";
+	const std::string gk = d->dyn ? "gemv_dyn_kernel<" : legacy ? "gemv_stream_kernel<" : "gemv_rb_kernel<";
 	switch (kernel_id) {
 	case 6:
 		s = std::string("engine_kernel<") + wt + ", ";
