@@ -182,15 +182,17 @@ int main(int argc, char **argv) {
 		bool two;
 		bool graph;
 		void (*rfn)(Args4) = nullptr; // roles-in-one-grid kernel (one launch per layer)
+		bool nopoll = false;          // serial launches without the flag poll (the launch path today)
 	};
 	std::vector<Cfg> cfgs = {
+	    {"serial nopoll lds 96K", phase_kernel<4, 0>, 96 * 1024, false, false, nullptr, true},
+	    {"serial nopoll graph  ", phase_kernel<4, 0>, 96 * 1024, false, true, nullptr, true},
 	    {"serial   P=0  lds 96K", phase_kernel<4, 0>, 96 * 1024, false, false},
 	    {"overlap  P=0  lds 96K", phase_kernel<4, 0>, 96 * 1024, true, false},
 	    {"overlap  P=8  lds 96K", phase_kernel<4, 8>, 96 * 1024, true, false},
 	    {"overlap  P=16 lds 96K", phase_kernel<4, 16>, 96 * 1024, true, false},
 	    {"overlap  P=16 lds 20K", phase_kernel<4, 16>, 20 * 1024, true, false},
 	    {"serial   P=0  graph  ", phase_kernel<4, 0>, 96 * 1024, false, true},
-	    {"overlap  P=16 graph  ", phase_kernel<4, 16>, 96 * 1024, true, true},
 	    {"roles    P=0  lds 64K", nullptr, 64 * 1024, false, false, roles_kernel<4, 0>},
 	    {"roles    P=8  lds 64K", nullptr, 64 * 1024, false, false, roles_kernel<4, 8>},
 	    {"roles    P=16 lds 64K", nullptr, 64 * 1024, false, false, roles_kernel<4, 16>},
@@ -217,7 +219,7 @@ int main(int argc, char **argv) {
 					off += sz[q];
 				a.w = w + off;
 				a.bytes = sz[p];
-				a.prev = k > 0 ? flags + (size_t)(k - 1) * NB : nullptr;
+				a.prev = k > 0 && !c.nopoll ? flags + (size_t)(k - 1) * NB : nullptr;
 				a.mine = flags + (size_t)k * NB;
 				a.act_in = act + (k & 1) * 4096;
 				a.act_out = act + ((k + 1) & 1) * 4096;

@@ -62,6 +62,8 @@ struct AttnWoArgs {
 	unsigned long long *trace; // [grid][4] s_memrealtime stamps (YALM_ATTN_WO_TRACE=1) or null
 	int win;            // Wo loads in flight per lane: 0 = all at once, 8 / 16 / 24 (YALM_ATTN_WO_WIN);
 	                    // -1 = no weight loads (YALM_ABLATE bit 32, timing only: results wrong)
+	int delay;          // s_memrealtime ticks (10 ns) the Wo workgroups wait before their slice loads
+	                    // (YALM_ATTN_WO_DELAY, tuning knob: lets the attention chain start alone)
 };
 
 // Gather this lane's XS pieces of the attention output (EPL floats each, pieces
@@ -160,6 +162,11 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 	// bounds (unconditional loads); rows below row0 belong to workgroup j - 1
 	const int lrow0 = min(row0, p.dim - AWO_RPW);
 	const char *wbase = p.wo + (size_t)lrow0 * p.q_dim * WT::BYTES;
+	if (p.delay > 0) {
+		const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+		while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)p.delay)
+			__builtin_amdgcn_s_sleep(2);
+	}
 	u32x4_t wr[LPT];
 	// p.win > 0: at most win loads in flight per lane (a sliding window), so the
 	// slice does not fill the CU's memory queues ahead of the attention's loads

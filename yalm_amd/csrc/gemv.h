@@ -264,6 +264,75 @@ __device__ __forceinline__ void stage_x(float *xs, const float *__restrict__ x, 
 	__syncthreads();
 }
 
+// x (and the norm weights) loaded into registers BEFORE the weight stream is
+// issued, so the staging does not wait behind the weight loads (vmcnt is in
+// order): XPRE<NORM> float4 per thread (2 with the norm weights, 4 without:
+// n <= 4 * XPRE * blockDim.x); finished by stage_x_regs.
+template <bool NORM>
+constexpr int xpre_n() {
+	return NORM ? 2 : 4;
+}
+template <bool NORM>
+struct XPre {
+	float4_t x[xpre_n<NORM>()], w[NORM ? xpre_n<NORM>() : 1];
+};
+template <bool NORM>
+__device__ __forceinline__ void prefetch_x(XPre<NORM> &r, const float *__restrict__ x, const float *__restrict__ normw,
+                                           int n) {
+	const int nthreads = blockDim.x;
+#pragma unroll
+	for (int k = 0; k < xpre_n<NORM>(); ++k) {
+		int i = (threadIdx.x + k * nthreads) * 4;
+		i = i < n ? i : n - 4; // unconditional (clamped) loads: no branch for hipcc to wait at
+		r.x[k] = *(const float4_t *)(x + i);
+		if constexpr (NORM)
+			r.w[k] = *(const float4_t *)(normw + i);
+	}
+}
+// infer.cpp:134-144 statement order, as stage_x
+template <bool NORM>
+__device__ __forceinline__ void stage_x_regs(float *xs, const XPre<NORM> &r, int n, float eps) {
+	const int tid = threadIdx.x;
+	const int nthreads = blockDim.x;
+	float scale = 1.0f;
+	if constexpr (NORM) {
+		float *red = xs + ((n + 3) & ~3);
+		float ss = 0.0f;
+#pragma unroll
+		for (int k = 0; k < xpre_n<NORM>(); ++k) {
+			if ((tid + k * nthreads) * 4 < n) {
+				const float4_t v = r.x[k];
+				ss += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+			}
+		}
+		ss = wave_sum(ss);
+		if ((tid & 63) == 0)
+			red[tid >> 6] = ss;
+		__syncthreads();
+		float tot = 0.0f;
+		for (int w = 0; w < nthreads / YALM_WAVE; ++w)
+			tot += red[w];
+		float rms = sqrtf(tot / n + eps);
+		scale = 1.0f / rms;
+	}
+#pragma unroll
+	for (int k = 0; k < xpre_n<NORM>(); ++k) {
+		const int i = (tid + k * nthreads) * 4;
+		if (i < n) {
+			float4_t v = r.x[k];
+			if constexpr (NORM) {
+				const float4_t w = r.w[k];
+				v[0] = v[0] * scale * w[0];
+				v[1] = v[1] * scale * w[1];
+				v[2] = v[2] * scale * w[2];
+				v[3] = v[3] * scale * w[3];
+			}
+			*(float4_t *)(xs + i) = v;
+		}
+	}
+	__syncthreads();
+}
+
 template <class WT, int R>
 __device__ __forceinline__ void fma_chunk(float (&acc)[R], const u32x4_t (&w)[R], const float *xs_lane) {
 	constexpr int EPL = WT::EPL;
@@ -504,6 +573,10 @@ __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__re
 
 	int ivr = wave / nch, ic = wave - (wave / nch) * nch; // issue cursor
 	const int vr0 = ivr, c0 = ic;
+	const bool xregs = n <= 4 * xpre_n<NORM>() * THREADS; // x (+ norm weights) fit the registers
+	XPre<NORM> xp;
+	if (xregs)
+		prefetch_x<NORM>(xp, x, normw, n); // ahead of the weight stream in vmcnt order
 	u32x4_t buf[U];
 #pragma unroll
 	for (int u = 0; u < U; ++u) {
@@ -513,7 +586,10 @@ __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__re
 	p.prologue();
 	for (int i = threadIdx.x; i < ngl * R * W; i += THREADS)
 		part[i] = 0.0f;
-	stage_x<NORM>(xs, x, normw, n, eps);
+	if (xregs)
+		stage_x_regs<NORM>(xs, xp, n, eps);
+	else
+		stage_x<NORM>(xs, x, normw, n, eps);
 
 	if (mine > 0) {
 		int cvr = vr0, cc = c0, cur = vr0; // consume cursor, row being accumulated

@@ -426,6 +426,8 @@ static int attn_wo_init(yalm_decoder_s *d) {
 		return YALM_ERR_ARG;
 	}
 	d->awo_win = d->ablate & 32 ? -1 : win; // ablation bit 32: no Wo weight loads (timing only)
+	const char *denv = getenv("YALM_ATTN_WO_DELAY");
+	d->awo_delay = denv ? std::max(0, atoi(denv)) : 0;
 	const char *tenv = getenv("YALM_ATTN_WO_TRACE");
 	if (tenv && atoi(tenv) != 0)
 		TRY(dalloc(d, (void **)&d->awo_trace, sizeof(unsigned long long) * 4 * d->awo_nb));
@@ -469,6 +471,7 @@ static int launch_attn_wo(yalm_decoder_s *d, const yalm_block_weights &w, int la
 	p.err = d->awo_err;
 	p.trace = d->awo_trace;
 	p.win = d->awo_win;
+	p.delay = d->awo_delay;
 	const int G = c.n_heads / c.n_kv_heads;
 	if constexpr (WT::BYTES == 2 || WT::BYTES == 1) {
 		if (p.q_dim * WT::BYTES == 4096)
