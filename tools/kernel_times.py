@@ -22,19 +22,20 @@ def main():
     ap.add_argument("--model", default="mistral-7b")
     ap.add_argument("--dtype", default="fp16", choices=["fp16", "fp8"])
     ap.add_argument("--iters", type=int, default=64)
+    ap.add_argument("--ctx", type=int, default=16, help="positions hydrated first (attention kv_len = ctx + 1)")
     args = ap.parse_args()
     runtime.check(runtime.lib.yalm_set_device(0))
     cfg = M.PRESETS[args.model].with_(weight_dtype=M.F16 if args.dtype == "fp16" else M.F8E5M2)
     dm = runtime.DeviceModel.synthetic(cfg, seed=1)
     dec = runtime.Decoder(dm)
-    for pos in range(16):
+    for pos in range(args.ctx):
         dec.forward((7 * pos + 1) % cfg.vocab_size, pos, runtime.HYDRATE_KV_CACHE)
     wb = M.DTYPE_BYTES[cfg.weight_dtype]
     nbytes = {0: (cfg.q_dim + 2 * cfg.kv_dim) * cfg.dim * wb, 2: cfg.dim * cfg.q_dim * wb,
               3: 2 * cfg.hidden_dim * cfg.dim * wb, 4: cfg.dim * cfg.hidden_dim * wb,
               5: cfg.vocab_size * cfg.dim * wb, 7: 3 * cfg.hidden_dim * cfg.dim * wb}
     env = {k: v for k, v in os.environ.items() if k.startswith("YALM_")}
-    print(f"[{args.model} {args.dtype}] {env}")
+    print(f"[{args.model} {args.dtype} kv_len {args.ctx + 1}] {env}")
     for kid, name in KINDS.items():
         if kid == 7 and not dec.ffn:
             continue

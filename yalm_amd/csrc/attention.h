@@ -46,14 +46,18 @@ __device__ __forceinline__ float ld_sc1(const float *p) {
 	return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// head outputs: plain stores for the next launch, write-through (sc1) when other
-// workgroups of the same launch read them (attn_wo.h)
-template <bool SC1>
-__device__ __forceinline__ void attn_out(float *p, float v) {
-	if constexpr (SC1)
-		st_sc1(p, v);
-	else
-		*p = v;
+// head outputs: plain stores for the next launch (GRAN = false), or, when other
+// workgroups of the same launch consume them (attn_wo.h), one 8-byte {value, tag}
+// granule per element written by ONE sc1 store, so that the data is its own
+// ready flag (MI355X_MICROARCH.md §visibility, R2 granules: no drain, no flag).
+template <bool GRAN>
+__device__ __forceinline__ void attn_out(float *out, size_t i, float v, unsigned tag) {
+	if constexpr (GRAN) {
+		const unsigned long long g = (unsigned long long)__float_as_uint(v) | ((unsigned long long)tag << 32);
+		__hip_atomic_store((unsigned long long *)out + i, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	} else {
+		out[i] = v;
+	}
 }
 
 // One workgroup's share of the split-KV attention: kv head g, key chunks s0,
@@ -62,13 +66,15 @@ __device__ __forceinline__ void attn_out(float *p, float v) {
 // Returns true on the workgroup that wrote the final head outputs of kv head g
 // (the single-chunk writer or the last arriver); the result is workgroup-uniform.
 // D = head_dim (multiple of 8, D/8 a power of two <= 64); GT >= G.
-template <int D, int GT, bool SC1OUT, class Hook>
+// GRAN: outputs as {value, tag} granules into `out` read as unsigned long long[].
+template <int D, int GT, bool GRAN, class Hook>
 // (no __restrict__ here: with it the K/V and q loads may legally sink below the
 // hook's asm barrier once inlined; the standalone kernel keeps it on its arguments)
 __device__ __forceinline__ bool attn_decode_body(bool active, int g, int s0, int S, const float *q, const uint16_t *kc,
                                                  const uint16_t *vc, const StepState *step, int n_heads,
                                                  int n_kv_heads, int max_seq_len, int nsplit, float *part,
-                                                 unsigned *counters, float *out, float *att_dbg, Hook &&hook) {
+                                                 unsigned *counters, float *out, float *att_dbg, Hook &&hook,
+                                                 unsigned gtag = 0) {
 	constexpr int CHUNK = attn_chunk<D>();
 	constexpr int LPK = D / 8;                     // lanes per K/V row, 16 B each
 	constexpr int KPW = 64 / LPK;                  // rows per wave-instruction
@@ -226,7 +232,7 @@ __device__ __forceinline__ bool attn_decode_body(bool active, int g, int s0, int
 #pragma unroll
 				for (int w = 0; w < ATTN_WAVES * KPW; ++w)
 					o += red[w][h][d];
-				attn_out<SC1OUT>(out + (size_t)(g * G + h) * D + d, o / ml[h][1]);
+				attn_out<GRAN>(out, (size_t)(g * G + h) * D + d, o / ml[h][1], gtag);
 			}
 			if (att_dbg) {
 				for (int i = tid; i < G * nt; i += ATTN_THREADS) {
@@ -317,7 +323,7 @@ __device__ __forceinline__ bool attn_decode_body(bool active, int g, int s0, int
 		if (dl) {
 #pragma unroll
 			for (int k = 0; k < DPL; ++k)
-				attn_out<SC1OUT>(out + (size_t)(g * G + h) * D + lane + 64 * k, o[k] / L);
+				attn_out<GRAN>(out, (size_t)(g * G + h) * D + lane + 64 * k, o[k] / L, gtag);
 		}
 		if (att_dbg) {
 			for (int t = lane; t < kv_len; t += 64) {

@@ -5,35 +5,31 @@
 // carries only the (small) KV read, and the Wo GEMV that follows starts its
 // 33.5 MB stream (Mistral-7B fp16) from a cold pipe. Here one grid holds two
 // kinds of workgroups:
-//   * ATTENTION workgroups [0, n_kv * S): attn_decode_body (attention.h) with
-//     write-through (sc1) head outputs; the workgroup that finishes kv head g
-//     (single-chunk writer or last arriver) drains its stores (vmcnt(0)), joins
-//     a workgroup barrier and stores the launch epoch (StepState::epoch) into
-//     every replica of kv head g's done flag (one wave instruction, 8 lanes, sc1
-//     stores). They issue no weight loads: a
-//     weight stream queued in front of the merge's loads (vmcnt is in order)
-//     would hold the whole hand-off behind it.
+//   * ATTENTION workgroups [0, n_kv * S): attn_decode_body (attention.h); the
+//     workgroup that finishes kv head g (single-chunk writer or last arriver of
+//     the split-KV merge) writes each head-output element as an 8-byte
+//     {value, epoch} GRANULE with ONE sc1 store into this layer's granule buffer:
+//     the data is its own ready flag (MI355X_MICROARCH.md §visibility, R2
+//     granule), so there is no drain (vmcnt(0)) and no separate flag store.
+//     They issue no weight loads: a weight stream queued in front of the merge's
+//     loads (vmcnt is in order) would hold the whole hand-off behind it.
 //   * Wo workgroups [n_kv * S, grid): each owns AWO_RPW contiguous Wo rows and
 //     issues them as register loads at once, so the 33.5 MB stream runs while
-//     the attention works. Each WAVE then takes its input pieces in turn: its
-//     lane 0 polls the XCD replica of the done flag of every kv head the
-//     piece's columns cover until it holds this launch's epoch (sc1 loads,
-//     bounded), the wave gathers the piece with 16-byte sc1 loads and dots it
-//     into every resident row (MI355X_MICROARCH.md §visibility, "Valid forms"
-//     row 1: one flag per producer, kept in R = 8 replicas on lines of their
-//     own), so a wave works as soon as ITS
-//     heads are done; then the rows are reduced across the workgroup in a
-//     fixed order and added to the residual (fused_matmul_add_residuals,
-//     infer.cu:270).
+//     the attention works. Each WAVE then gathers its input columns' granules
+//     with 16-byte sc1 loads (two granules each), re-reading a batch until every
+//     tag in the wave holds this launch's epoch (bounded), so a wave works as
+//     soon as ITS heads are done; it dots the columns into every resident row;
+//     the rows are reduced across the workgroup in a fixed order and added to
+//     the residual (fused_matmul_add_residuals, infer.cu:270).
+// Round 1 handed off through per-kv-head done flags (writer: drain, barrier,
+// flag; reader: poll, then gather): two more serialised memory round trips.
 // Workgroups dispatch in index order, so every attention workgroup is resident
 // before any Wo workgroup spins, and attention never waits on Wo: no deadlock
-// even when the grid is not co-resident. Flags: one slot of n_kv x 8 replicas
-// per layer, each holding the epoch of the last launch that finished that kv
-// head. The epoch grows by one per forward and per yalm_block call, so a flag
-// is never reset and any order of layer launches (one layer repeated, a forward
-// stopped part-way) stays correct; there is no in-launch reset ticket either (a
-// returning atomic from every workgroup costs ~6 us of serialised fan-in,
-// MI355X_MICROARCH.md row fanin). Every spin is bounded and reports in *err.
+// even when the grid is not co-resident. Tags: the epoch grows by one per
+// forward and per yalm_block call and each layer has its own buffer, so a
+// granule is never reset and any order of layer launches (one layer repeated, a
+// forward stopped part-way) stays correct. Every spin is bounded and reports in
+// *err.
 //
 // Geometry: Wo rows are q_dim * BYTES = XS * 4 KB (XS in {1, 2}); Wo workgroup
 // j owns rows [j * AWO_RPW, j * AWO_RPW + AWO_RPW) and thread t loads 16-byte
@@ -45,19 +41,16 @@
 
 #define AWO_RPW 16                   // Wo rows per Wo workgroup (256 of them for Mistral-7B)
 #define AWO_TIMEOUT 200000000ull     // 2 s of s_memrealtime (100 MHz)
-#define AWO_REPL 8                   // done-counter replicas (one per XCD)
-#define AWO_REPL_STRIDE 32           // words between replicas (128-B lines of their own)
-#define AWO_HEAD (AWO_REPL * AWO_REPL_STRIDE) // words per kv head's counter; a layer slot is n_kv of them
+#define AWO_REPL_STRIDE 32           // words of the error slot (a 128-B line of its own)
 
 struct AttnWoArgs {
 	int n_heads, n_kv, max_seq_len, nsplit, S; // S = key-chunk splits per kv head: n_kv * S attention workgroups
 	int q_dim, dim;
 	float *part;        // attention chunk partials (n_heads, nsplit, D + 2)
 	unsigned *counters; // per-kv-head arrival tickets (attention.h)
-	float *att;         // attention output (q_dim), written sc1
+	const unsigned long long *gran; // this layer's attention output (q_dim) as {value, epoch} granules
 	const char *wo;     // Wo (dim, q_dim)
 	float *x;           // residual stream (dim)
-	unsigned *done;     // this layer's per-kv-head done flags: [n_kv][AWO_REPL replicas, AWO_REPL_STRIDE words apart]
 	unsigned *err;      // error bits (bounded spin gave up)
 	unsigned long long *trace; // [grid][4] s_memrealtime stamps (YALM_ATTN_WO_TRACE=1) or null
 	int win;            // Wo loads in flight per lane: 0 = all at once, 8 / 16 / 24 (YALM_ATTN_WO_WIN);
@@ -66,58 +59,94 @@ struct AttnWoArgs {
 	                    // (YALM_ATTN_WO_DELAY, tuning knob: lets the attention chain start alone)
 };
 
-// Gather this lane's XS pieces of the attention output (EPL floats each, pieces
-// 256 * EPL floats apart) with 16-byte sc1 loads -- the hand-off's load form
-// (4- or 16-byte sc1 loads). 4-byte loads at a 32-byte lane stride made every
-// wave instruction request 16 lines for 256 useful bytes, 8 times over, from all
-// 256 Wo workgroups at once. hipcc does not track asm loads: one statement issues
-// them all and drains vmcnt (the weight slice has landed by then anyway).
+// Eight 16-byte sc1 loads from arbitrary addresses in one statement, one vmcnt(0)
+// (hipcc does not track asm loads: the statement drains its own).
+__device__ __forceinline__ void awo_ld8_sc1(u32x4_t (&v)[8], const void *const (&a)[8]) {
+	asm volatile("global_load_dwordx4 %0, %8, off sc1\n\t"
+	             "global_load_dwordx4 %1, %9, off sc1\n\t"
+	             "global_load_dwordx4 %2, %10, off sc1\n\t"
+	             "global_load_dwordx4 %3, %11, off sc1\n\t"
+	             "global_load_dwordx4 %4, %12, off sc1\n\t"
+	             "global_load_dwordx4 %5, %13, off sc1\n\t"
+	             "global_load_dwordx4 %6, %14, off sc1\n\t"
+	             "global_load_dwordx4 %7, %15, off sc1\n\t"
+	             "s_waitcnt vmcnt(0)"
+	             : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]),
+	               "=&v"(v[7])
+	             : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7])
+	             : "memory");
+}
+
+// This lane's XS pieces of the attention output (EPL columns each, pieces
+// ATTN_THREADS * EPL columns apart) as {value, tag} granules: first one sentinel
+// granule per covered head is polled, then 16-byte sc1 loads (two granules each)
+// in batches of 8, each batch re-read until all its tags equal `tag` across the
+// wave (the check that makes it correct). False if the bounded spin gave up
+// (deadline, s_memrealtime).
 template <int EPL, int XS>
-__device__ __forceinline__ void awo_gather(float (&xs)[XS][EPL], const float *src) {
-	constexpr int NL = XS * EPL / 4; // 16-byte loads per lane: 2, 4 or 8
-	static_assert(NL == 2 || NL == 4 || NL == 8, "EPL * XS in {8, 16, 32}");
-	constexpr int LPP = EPL / 4;      // loads per piece
-	const float *a[8];
-#pragma unroll
-	for (int i = 0; i < NL; ++i)
-		a[i] = src + (size_t)(i / LPP) * ATTN_THREADS * EPL + (i % LPP) * 4;
-	u32x4_t v[8];
-	if constexpr (NL == 2) {
-		asm volatile("global_load_dwordx4 %0, %2, off sc1\n\t"
-		             "global_load_dwordx4 %1, %3, off sc1\n\t"
-		             "s_waitcnt vmcnt(0)"
-		             : "=&v"(v[0]), "=&v"(v[1])
-		             : "v"(a[0]), "v"(a[1])
-		             : "memory");
-	} else if constexpr (NL == 4) {
-		asm volatile("global_load_dwordx4 %0, %4, off sc1\n\t"
-		             "global_load_dwordx4 %1, %5, off sc1\n\t"
-		             "global_load_dwordx4 %2, %6, off sc1\n\t"
-		             "global_load_dwordx4 %3, %7, off sc1\n\t"
-		             "s_waitcnt vmcnt(0)"
-		             : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3])
-		             : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3])
-		             : "memory");
-	} else {
-		asm volatile("global_load_dwordx4 %0, %8, off sc1\n\t"
-		             "global_load_dwordx4 %1, %9, off sc1\n\t"
-		             "global_load_dwordx4 %2, %10, off sc1\n\t"
-		             "global_load_dwordx4 %3, %11, off sc1\n\t"
-		             "global_load_dwordx4 %4, %12, off sc1\n\t"
-		             "global_load_dwordx4 %5, %13, off sc1\n\t"
-		             "global_load_dwordx4 %6, %14, off sc1\n\t"
-		             "global_load_dwordx4 %7, %15, off sc1\n\t"
-		             "s_waitcnt vmcnt(0)"
-		             : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]),
-		               "=&v"(v[7])
-		             : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7])
-		             : "memory");
+__device__ __forceinline__ bool awo_gather_gran(float (&xs)[XS][EPL], const unsigned long long *gran, int tid,
+                                                unsigned tag, unsigned long long deadline) {
+	constexpr int LPP = EPL / 2;   // 16-byte loads per piece
+	constexpr int NL = XS * LPP;   // 4, 8 or 16
+	constexpr int NB = (NL + 7) / 8;
+	constexpr int D = 128;
+	constexpr int HPP = 64 * EPL / D; // heads per piece (4 or 8)
+	bool alive = true;
+	// cheap wait first: one lane per covered head polls that head's last granule
+	// (one 8-byte sc1 load per lane), so the full re-reads below run ~once
+	{
+		const int lane = tid & 63, wave = tid >> 6;
+		const int l = lane < XS * HPP ? lane : 0;
+		const int k = l / HPP;
+		const int h = (k * ATTN_THREADS + 64 * wave) * EPL / D + l % HPP;
+		const unsigned long long *sent = gran + (size_t)h * D + (D - 1);
+		for (;;) {
+			const unsigned long long g = __hip_atomic_load(sent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			if (__all((unsigned)(g >> 32) == tag))
+				break;
+			__builtin_amdgcn_s_sleep(1);
+			if (__builtin_amdgcn_s_memrealtime() > deadline) {
+				alive = false;
+				break;
+			}
+		}
 	}
 #pragma unroll
-	for (int i = 0; i < NL * 4; ++i) {
-		const uint32_t w = v[i / 4][i % 4];
-		xs[i / EPL][i % EPL] = __uint_as_float(w);
+	for (int bt = 0; bt < NB; ++bt) {
+		const void *a[8];
+#pragma unroll
+		for (int i = 0; i < 8; ++i) {
+			const int l = bt * 8 + (i < NL - bt * 8 ? i : 0); // pad a short batch with a repeat
+			const int k = l / LPP, e = (l % LPP) * 2;
+			a[i] = gran + (size_t)(k * ATTN_THREADS + tid) * EPL + e;
+		}
+		u32x4_t v[8];
+		for (;;) {
+			awo_ld8_sc1(v, a);
+			bool ok = true;
+#pragma unroll
+			for (int i = 0; i < 8; ++i) {
+				const uint32_t t0 = v[i][1], t1 = v[i][3];
+				ok = ok && t0 == tag && t1 == tag;
+			}
+			if (__all(ok) || !alive)
+				break;
+			__builtin_amdgcn_s_sleep(1);
+			if (__builtin_amdgcn_s_memrealtime() > deadline)
+				alive = false; // one more pass, then give up (results wrong, reported)
+		}
+#pragma unroll
+		for (int i = 0; i < 8; ++i) {
+			if (i < NL - bt * 8) {
+				const int l = bt * 8 + i;
+				const int k = l / LPP, e = (l % LPP) * 2;
+				const uint32_t w0 = v[i][0], w1 = v[i][2];
+				xs[k][e] = __uint_as_float(w0);
+				xs[k][e + 1] = __uint_as_float(w1);
+			}
+		}
 	}
+	return alive;
 }
 
 template <class WT, int GT, int XS>
@@ -139,16 +168,9 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 	if (b < units) { // ---- attention workgroup
 		const bool wrote = attn_decode_body<D, GT, true>(true, b % p.n_kv, b / p.n_kv, p.S, q, kc, vc, step,
 		                                                 p.n_heads, p.n_kv, p.max_seq_len, p.nsplit, p.part,
-		                                                 p.counters, p.att, nullptr, [] {});
-		if (wrote) {
-			asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // every storing wave drains its sc1 stores
-			__syncthreads();
-			if (tid < AWO_REPL) // kv head b % n_kv done: one wave instruction, one lane per replica
-				__hip_atomic_store(&p.done[(b % p.n_kv) * AWO_HEAD + tid * AWO_REPL_STRIDE], epoch, __ATOMIC_RELAXED,
-				                   __HIP_MEMORY_SCOPE_AGENT);
-			if (tr)
-				tr[1] = __builtin_amdgcn_s_memrealtime();
-		}
+		                                                 p.counters, (float *)p.gran, nullptr, [] {}, epoch);
+		if (wrote && tr) // the head outputs are their own ready flags: nothing to drain or signal
+			tr[1] = __builtin_amdgcn_s_memrealtime();
 		if (tr)
 			tr[3] = __builtin_amdgcn_s_memrealtime();
 		return;
@@ -187,37 +209,15 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 		tr[1] = __builtin_amdgcn_s_memrealtime();
 	}
 
-	// ---- per wave: wait for every kv head its input pieces cover (piece k's 64 * EPL
-	// columns span q heads e0 / D .. and kv groups / G), then gather all pieces at
-	// once with 16-byte sc1 loads (one round trip) and dot them into every resident
-	// row. The polling lane's wave loads only after its polls matched
-	// (MI355X_MICROARCH.md §visibility "Valid forms" row 2).
-	const int G = p.n_heads / p.n_kv;
-	const int rep = (b % AWO_REPL) * AWO_REPL_STRIDE;
-	if (lane == 0) {
-		const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-		bool dead = false;
-#pragma unroll
-		for (int k = 0; k < XS; ++k) {
-			const int e0 = (k * ATTN_THREADS + 64 * wave) * EPL;
-			const int g_lo = e0 / D / G, g_hi = (e0 + 64 * EPL - 1) / D / G;
-			for (int g = g_lo; g <= g_hi && !dead; ++g) {
-				const unsigned *c = p.done + g * AWO_HEAD + rep;
-				while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-					__builtin_amdgcn_s_sleep(1);
-					if (__builtin_amdgcn_s_memrealtime() - t0 > AWO_TIMEOUT) {
-						__hip_atomic_fetch_or(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-						dead = true;
-						break;
-					}
-				}
-			}
-		}
-	}
+	// ---- per wave: gather this lane's input columns as {value, tag} granules with
+	// 16-byte sc1 loads until every tag holds this launch's epoch (each wave waits
+	// only for the heads its columns cover), then dot them into every resident row.
+	const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+	float xs[XS][EPL];
+	if (!awo_gather_gran<EPL, XS>(xs, p.gran, tid, epoch, t0 + AWO_TIMEOUT) && lane == 0)
+		__hip_atomic_fetch_or(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 	if (tr)
 		tr[2] = __builtin_amdgcn_s_memrealtime();
-	float xs[XS][EPL];
-	awo_gather<EPL, XS>(xs, p.att + (size_t)tid * EPL);
 	float a0[AWO_RPW], a1[AWO_RPW];
 #pragma unroll
 	for (int r = 0; r < AWO_RPW; ++r) {

@@ -136,8 +136,8 @@ struct yalm_decoder_s {
 	unsigned long long *awo_trace = nullptr; // YALM_ATTN_WO_TRACE=1: [grid][4] stamps of the last launch
 	int awo_win = 0;                 // Wo loads in flight per lane (YALM_ATTN_WO_WIN), -1 = none (ablation)
 	int awo_delay = 0;               // ticks the Wo workgroups wait before their slice loads (YALM_ATTN_WO_DELAY)
-	unsigned *awo_sync = nullptr;    // [n_layers][n_kv][AWO_HEAD] per-kv-head done flags (epochs), then the error word
-	unsigned *awo_err = nullptr;     // = awo_sync + n_layers * n_kv * AWO_HEAD
+	unsigned long long *awo_gran = nullptr; // [n_layers][q_dim] attention outputs as {value, epoch} granules
+	unsigned *awo_err = nullptr;     // error word (bounded spins that gave up)
 	// launch path: rmsnorm + GLU + W2 + residual as one launch (ffn.h) when
 	// supported; YALM_FFN=0 selects the separate GLU and W2 kernels
 	bool ffn = false;

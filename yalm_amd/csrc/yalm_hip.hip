@@ -403,7 +403,7 @@ static int attn_wo_init(yalm_decoder_s *d) {
 	const int rb = c.n_heads * c.head_dim * (c.weight_dtype == YALM_F16 ? 2 : 1);
 	if (rb != 4096 && rb != 8192)
 		return YALM_OK;
-	if (c.dim < AWO_RPW || c.n_kv_heads * AWO_REPL > ATTN_THREADS)
+	if (c.dim < AWO_RPW)
 		return YALM_OK;
 	int occ = 0; // the Wo workgroups spin, but only on attention workgroups dispatched before them
 	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, attn_wo_pick(c.weight_dtype, G, rb / 4096), ATTN_THREADS,
@@ -411,9 +411,11 @@ static int attn_wo_init(yalm_decoder_s *d) {
 	    occ < 1)
 		return YALM_OK;
 	const int nchunks = (c.max_seq_len + attn_chunk<128>() - 1) / attn_chunk<128>();
-	const size_t slot = (size_t)c.n_kv_heads * AWO_HEAD; // per layer: one counter per kv head
-	TRY(dalloc(d, (void **)&d->awo_sync, sizeof(unsigned) * (c.n_layers * slot + AWO_REPL_STRIDE)));
-	d->awo_err = d->awo_sync + c.n_layers * slot;
+	// per layer: the attention output as {value, epoch} granules (zero tags never match:
+	// the epoch is >= 1 from the first forward / yalm_block on), then the error word
+	const size_t gran = (size_t)c.n_layers * c.n_heads * c.head_dim;
+	TRY(dalloc(d, (void **)&d->awo_gran, sizeof(unsigned long long) * gran));
+	TRY(dalloc(d, (void **)&d->awo_err, sizeof(unsigned) * AWO_REPL_STRIDE));
 	// key-chunk splits per kv head, as the standalone attention launch (YALM_AWO_SPLITS: sweep knob)
 	const char *senv = getenv("YALM_AWO_SPLITS");
 	d->awo_S = std::min(nchunks, senv ? std::max(1, atoi(senv)) : 32);
@@ -463,11 +465,9 @@ static int launch_attn_wo(yalm_decoder_s *d, const yalm_block_weights &w, int la
 	p.dim = c.dim;
 	p.part = d->part;
 	p.counters = d->attn_counters;
-	p.att = d->xb2;
+	p.gran = d->awo_gran + (size_t)layer * p.q_dim;
 	p.wo = (const char *)w.wo;
 	p.x = d->x;
-	const size_t slot = (size_t)c.n_kv_heads * AWO_HEAD;
-	p.done = d->awo_sync + (size_t)layer * slot;
 	p.err = d->awo_err;
 	p.trace = d->awo_trace;
 	p.win = d->awo_win;
