@@ -4,7 +4,7 @@ CXX ?= g++
 ARCH ?= gfx950
 HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall
 CSRC = yalm_amd/csrc
-HIP_SRCS = $(CSRC)/yalm_hip.hip $(CSRC)/prefill.hip $(CSRC)/engine.hip $(CSRC)/dyn.hip
+HIP_SRCS = $(CSRC)/yalm_hip.hip $(CSRC)/prefill.hip $(CSRC)/engine.hip $(CSRC)/dyn.hip $(CSRC)/awl.hip
 HIP_OBJS = $(patsubst $(CSRC)/%.hip,build/%.o,$(HIP_SRCS))
 HIP_HDRS = $(wildcard $(CSRC)/*.h) include/yalm_hip.h
 

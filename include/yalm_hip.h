@@ -137,8 +137,9 @@ int yalm_get_logits(yalm_decoder d, float *host);
  * GEMV, 1 = attention, 2 = Wo GEMV, 3 = W1/W3 GEMV+GLU, 4 = W2 GEMV,
  * 5 = logits GEMV, 6 = the whole-token engine launch (greedy mode; advances
  * the decoder's device step), 7 = the fused feed-forward launch (rmsnorm + W1/W3
- * + GLU + W2 + residual, yalm_decoder_ffn). Used by bench.py for the roofline
- * of the dominant kernel. */
+ * + GLU + W2 + residual, yalm_decoder_ffn), 8 / 9 = the fused attention + Wo
+ * launch in its granule hand-off / short-context form (yalm_decoder_attn_wo).
+ * Used by bench.py for the roofline of the dominant kernel. */
 int yalm_time_kernel(yalm_decoder d, int kernel_id, int iters, float *avg_ms);
 /* Override the GEMV launch geometry of one weight-streaming kernel kind
  * (0 = QKV, 1 = Wo, 2 = W1/W3, 3 = W2, 4 = logits): workgroup size
@@ -160,7 +161,12 @@ int yalm_decoder_engine(yalm_decoder d);
  * residual add) as ONE launch (attn_wo.h: the Wo weight stream overlaps the
  * attention; replaces attn + fused_matmul_add_residuals, infer.cu:338-524, 270):
  * single GPU, head_dim 128, fp16 / fp8 weights with 4 or 8 KB Wo rows, and
- * YALM_ATTN_WO not 0 at creation. 0 = two separate launches. */
+ * YALM_ATTN_WO not 0 at creation. 0 = two separate launches.
+ * Two forms, picked per token from the position the host tracks (both correct
+ * at any kv_len): while kv_len <= YALM_AWO_LOCAL (opt-in, default 0 = never) every
+ * Wo workgroup recomputes the attention from the L2-resident KV cache
+ * (attn_wo_local_kernel, no cross-CU hand-off); longer contexts hand the split-KV
+ * attention output to the Wo workgroups as {value, epoch} granules. */
 int yalm_decoder_attn_wo(yalm_decoder d);
 /* Timeline of the most recent fused attention + Wo launch (decoder created with
  * YALM_ATTN_WO_TRACE=1): 4 s_memrealtime (100 MHz) stamps per workgroup at
@@ -169,6 +175,10 @@ int yalm_decoder_attn_wo(yalm_decoder d);
  * [0, *attention_workgroups) are attention, the rest Wo. */
 int yalm_attn_wo_trace(yalm_decoder d, unsigned long long *host, size_t count, int *workgroups,
                        int *attention_workgroups);
+/* The same for the short-context form (attn_wo_local_kernel, one workgroup per 16
+ * Wo rows): start, attention output in LDS, Wo slice landed (the trace waits for
+ * it), end. */
+int yalm_attn_wo_local_trace(yalm_decoder d, unsigned long long *host, size_t count, int *workgroups);
 /* 1 if this decoder's launch path runs the whole feed-forward half of a block
  * (rmsnorm, W1/W3 + SiLU/GELU-GLU, W2 + residual; infer.cu:598-620 + 270-288,
  * which the reference launches as three kernels) as ONE launch (ffn.h: the W2

@@ -44,30 +44,46 @@ def relerr(a, b):
     return float(np.max(np.abs(a - b)) / (np.max(np.abs(b)) + 1e-30))
 
 
-def make(cfg, seed, fused=True, t=None):
+# short-context form (attn_wo_local_kernel, opt-in) selection: "auto" = the form
+# switches at kv_len 64 (inside one sequence at max_seq_len 72), "never" = granule
+# hand-off form only (the default), "always" = the short-context form at every
+# kv_len (its 32-key block loop)
+LOCAL = {"default": None, "auto": "64", "never": "0", "always": "1000000"}
+
+
+def make(cfg, seed, fused=True, t=None, local="default"):
     runtime = rt()
     if t is None:
         t = M.synth_host_tensors(cfg, seed=seed)
     dm = runtime.DeviceModel.from_arrays(cfg, t)
-    old = os.environ.get("YALM_ATTN_WO")
-    os.environ["YALM_ATTN_WO"] = "1" if fused else "0"
+    env = {"YALM_ATTN_WO": "1" if fused else "0", "YALM_AWO_LOCAL": LOCAL[local]}
+    old = {k: os.environ.get(k) for k in env}
+    for k, v in env.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
     try:
         dec = runtime.Decoder(dm)
     finally:
-        if old is None:
-            del os.environ["YALM_ATTN_WO"]
-        else:
-            os.environ["YALM_ATTN_WO"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     assert not dec.engine
     assert dec.attn_wo == fused
     return t, dm, dec
 
 
+@pytest.mark.parametrize("local", ["auto", "never", "always"])
 @pytest.mark.parametrize("name,cfg", CASES, ids=[c[0] for c in CASES])
-def test_attn_wo_forward_and_greedy_vs_oracle(name, cfg):
+def test_attn_wo_forward_and_greedy_vs_oracle(name, cfg, local):
     """OUTPUT-mode logits at every position (hydrated prompt first), through
-    pos >= max_seq_len (ring + sink rotation); then the device greedy loop."""
-    t, dm, dec = make(cfg, seed=5)
+    pos >= max_seq_len (ring + sink rotation); then the device greedy loop.
+    "auto" crosses from the short-context form (kv_len <= 64) to the granule
+    form (max_seq_len 72) inside one sequence."""
+    t, dm, dec = make(cfg, seed=5, local=local)
     om = O.OracleModel(cfg, t)
     try:
         prompt = [1, 17, 45, 99, 3]
@@ -92,11 +108,12 @@ def test_attn_wo_forward_and_greedy_vs_oracle(name, cfg):
         dm.close()
 
 
+@pytest.mark.parametrize("local", ["never", "always"])
 @pytest.mark.parametrize("name,cfg", CASES[:2] + CASES[4:5], ids=[c[0] for c in CASES[:2] + CASES[4:5]])
-def test_attn_wo_matches_separate_launches(name, cfg):
+def test_attn_wo_matches_separate_launches(name, cfg, local):
     """Same weights, same tokens: fused vs separate attention and Wo launches
     (the residual x after the whole forward and the logits), 40 positions."""
-    t, dm, dec = make(cfg, seed=7, fused=True)
+    t, dm, dec = make(cfg, seed=7, fused=True, local=local)
     _, dm2, dec2 = make(cfg, seed=7, fused=False, t=t)
     try:
         tok = 11
@@ -123,6 +140,73 @@ def test_attn_wo_long_context_split_attention():
     try:
         n = 1100
         assert dec.generate_greedy(3, 0, n) == om.greedy(3, 0, n)
+    finally:
+        dec.close()
+        dm.close()
+
+
+def test_attn_wo_local_long_context():
+    """The short-context form forced at every kv_len (up to 300: ten 32-key
+    blocks with the online-softmax rescale, then the sliding window): greedy
+    tokens equal the oracle's."""
+    cfg = BASE.with_(n_layers=2, max_seq_len=300)
+    t, dm, dec = make(cfg, seed=13, local="always")
+    om = O.OracleModel(cfg, t)
+    try:
+        n = 330
+        assert dec.generate_greedy(3, 0, n) == om.greedy(3, 0, n)
+    finally:
+        dec.close()
+        dm.close()
+
+
+def test_attn_wo_forms_switch_in_greedy_loop():
+    """The host picks the form per replay from the position it tracks: one
+    greedy run across the threshold (kv_len 60 .. 71) equals the oracle, and so
+    does a run continued with enqueue_greedy after a forward."""
+    cfg = BASE
+    t, dm, dec = make(cfg, seed=14, local="auto")
+    om = O.OracleModel(cfg, t)
+    try:
+        assert dec.generate_greedy(9, 0, 70) == om.greedy(9, 0, 70)
+        tok, pos = 4, 50
+        lg = dec.forward(tok, pos)
+        lo = om.forward(tok, pos)
+        assert relerr(lg, lo) < 1e-3
+    finally:
+        dec.close()
+        dm.close()
+
+
+@pytest.mark.parametrize("local", ["never", "always"])
+def test_attn_wo_replay_deterministic_forms(local):
+    """Bitwise-identical logits for the same token sequence on two decoders,
+    for each form."""
+    outs = []
+    for _ in range(2):
+        t, dm, dec = make(BASE, seed=4, local=local)
+        try:
+            tok, got = 2, []
+            for pos in range(20):
+                lg = dec.forward(tok, pos)
+                got.append(lg)
+                tok = int(np.argmax(lg))
+            outs.append(np.concatenate([g.ravel() for g in got]))
+        finally:
+            dec.close()
+            dm.close()
+    np.testing.assert_array_equal(outs[0], outs[1])
+
+
+def test_attn_wo_time_kernel_both_forms():
+    """yalm_time_kernel ids 8 / 9 time the two forms of the fused launch."""
+    t, dm, dec = make(BASE, seed=3, local="auto")
+    try:
+        for pos in range(8):
+            dec.forward(1 + pos, pos, rt().HYDRATE_KV_CACHE)
+        for kid in (8, 9):
+            assert dec.time_kernel(kid, 4) > 0
+            assert "attn_wo" in dec.kernel_name(kid)
     finally:
         dec.close()
         dm.close()

@@ -246,3 +246,4 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 	if (tr)
 		tr[3] = __builtin_amdgcn_s_memrealtime();
 }
+

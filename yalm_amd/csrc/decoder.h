@@ -88,8 +88,10 @@ struct yalm_decoder_s {
 	int tokens_cap = 0;
 	float *logits_pinned = nullptr;
 	std::vector<void *> dev_allocs;
-	hipGraph_t graph[N_GRAPHS] = {};
-	hipGraphExec_t exec[N_GRAPHS] = {};
+	// [v][which]: v = 1 captures the short-context attention + Wo kernel (attn_wo_local_kernel)
+	hipGraph_t graph[2][N_GRAPHS] = {};
+	hipGraphExec_t exec[2][N_GRAPHS] = {};
+	long long host_pos = -1;         // position of the next forward as the host knows it (-1: unknown)
 	unsigned *attn_counters = nullptr; // per-kv-head arrival tickets (zeroed; the last arriver resets)
 	GemvCfg gemv[GK_N];
 	bool eager = false;     // YALM_EAGER=1: launch kernels directly (profilers that mis-handle graph replay)
@@ -138,6 +140,10 @@ struct yalm_decoder_s {
 	int awo_delay = 0;               // ticks the Wo workgroups wait before their slice loads (YALM_ATTN_WO_DELAY)
 	unsigned long long *awo_gran = nullptr; // [n_layers][q_dim] attention outputs as {value, epoch} granules
 	unsigned *awo_err = nullptr;     // error word (bounded spins that gave up)
+	int awo_local_max = 0;           // kv_len up to which the short-context kernel runs (YALM_AWO_LOCAL, 0 = never)
+	bool awo_local_now = false;      // the forward being enqueued uses attn_wo_local_kernel
+	int awl_kv_first = 1;            // YALM_AWL_KV_FIRST: K/V loads issued ahead of the Wo slice
+	unsigned long long *awl_trace = nullptr; // YALM_ATTN_WO_TRACE=1: [dim / 16][4] stamps of the last local launch
 	// launch path: rmsnorm + GLU + W2 + residual as one launch (ffn.h) when
 	// supported; YALM_FFN=0 selects the separate GLU and W2 kernels
 	bool ffn = false;
@@ -156,6 +162,10 @@ struct yalm_decoder_s {
 
 // ------------------------------------------------------------------ shared helpers
 int dalloc(yalm_decoder_s *d, void **p, size_t bytes); // zeroed device allocation owned by d
+
+// short-context fused attention + Wo (awl.hip, attn_wo_local.h)
+int attn_wo_local_occupancy(int dtype, int G, int XS); // workgroups per CU (0: not launchable)
+int launch_attn_wo_local(yalm_decoder_s *d, const yalm_block_weights &w);
 
 // persistent engine (engine.hip)
 int engine_init(yalm_decoder_s *d);                // enables d->engine when supported

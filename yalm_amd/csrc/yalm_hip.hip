@@ -388,7 +388,6 @@ static const void *attn_wo_pick(int dtype, int G, int XS) {
 		return XS == 1 ? attn_wo_fn_g<WF16, 1>(G) : attn_wo_fn_g<WF16, 2>(G);
 	return XS == 1 ? attn_wo_fn_g<WF8, 1>(G) : attn_wo_fn_g<WF8, 2>(G);
 }
-
 // Single-GPU decoders with head_dim 128, G <= 8 and fp16 / fp8 Wo rows of 4 or 8 KB.
 static int attn_wo_init(yalm_decoder_s *d) {
 	const yalm_config &c = d->c;
@@ -429,10 +428,28 @@ static int attn_wo_init(yalm_decoder_s *d) {
 	}
 	d->awo_win = d->ablate & 32 ? -1 : win; // ablation bit 32: no Wo weight loads (timing only)
 	const char *denv = getenv("YALM_ATTN_WO_DELAY");
-	d->awo_delay = denv ? std::max(0, atoi(denv)) : 0;
+	// default 0.2 us: the attention workgroups' K/V loads reach HBM ahead of the 33.5 MB Wo
+	// stream (tools/sweep_awo.sh, profiles/r2_sweep_awo_delay.txt: 10.6 -> 10.1 us at kv_len 17,
+	// 10.6 -> 10.4 at kv_len 151; 0.4-0.6 us delays lose it again at long contexts)
+	d->awo_delay = denv ? std::max(0, atoi(denv)) : 20;
 	const char *tenv = getenv("YALM_ATTN_WO_TRACE");
 	if (tenv && atoi(tenv) != 0)
 		TRY(dalloc(d, (void **)&d->awo_trace, sizeof(unsigned long long) * 4 * d->awo_nb));
+	// short-context form (attn_wo_local_kernel): every Wo workgroup recomputes the attention
+	// from L2 while its slice streams in; the host picks it per token while kv_len <= this
+	// (YALM_AWO_LOCAL, opt-in: 0 = never; any value is correct, the kernel loops over 32-key
+	// blocks). Measured slower on MI355X (Mistral-7B fp16, kv_len 17: 16-20 us per launch vs
+	// 10.7 for the granule form): 256 CUs each re-reading every head's K/V
+	// from L2 (~4 MB per XCD per 32-key block) and the replicated softmax cost more than
+	// the hand-off they remove.
+	const char *lenv = getenv("YALM_AWO_LOCAL");
+	d->awo_local_max = lenv ? std::max(0, atoi(lenv)) : 0;
+	const char *kfenv = getenv("YALM_AWL_KV_FIRST");
+	d->awl_kv_first = kfenv ? atoi(kfenv) != 0 : 1;
+	if (d->awo_local_max > 0 && attn_wo_local_occupancy(c.weight_dtype, G, rb / 4096) < 1)
+		d->awo_local_max = 0;
+	if (d->awo_local_max > 0 && tenv && atoi(tenv) != 0)
+		TRY(dalloc(d, (void **)&d->awl_trace, sizeof(unsigned long long) * 4 * ((c.dim + AWO_RPW - 1) / AWO_RPW)));
 	d->attn_wo = true;
 	return YALM_OK;
 }
@@ -454,6 +471,8 @@ static void launch_attn_wo_g(yalm_decoder_s *d, const yalm_block_weights &w, con
 }
 template <class WT>
 static int launch_attn_wo(yalm_decoder_s *d, const yalm_block_weights &w, int layer) {
+	if (d->awo_local_now)
+		return launch_attn_wo_local(d, w);
 	const yalm_config &c = d->c;
 	AttnWoArgs p;
 	p.n_heads = c.n_heads;
@@ -798,8 +817,18 @@ static int enqueue_forward(yalm_decoder_s *d, int which) {
 	return YALM_OK;
 }
 
+// Which attention + Wo form the forward at position pos runs (the host tracks the
+// position; both forms are correct at any kv_len, the choice is speed only).
+static bool use_local_at(const yalm_decoder_s *d, long long pos) {
+	if (!d->attn_wo || d->awo_local_max <= 0 || pos < 0)
+		return false;
+	const long long kv_len = pos >= d->c.max_seq_len ? d->c.max_seq_len : pos + 1;
+	return kv_len <= d->awo_local_max;
+}
+
 static int ensure_graph(yalm_decoder_s *d, int which) {
-	if (d->exec[which] || d->eager)
+	const int v = d->awo_local_now ? 1 : 0;
+	if (d->exec[v][which] || d->eager)
 		return YALM_OK;
 	HIPCHK(hipStreamBeginCapture(d->stream, hipStreamCaptureModeRelaxed));
 	int r = enqueue_forward(d, which);
@@ -808,9 +837,22 @@ static int ensure_graph(yalm_decoder_s *d, int which) {
 	if (r != YALM_OK)
 		return r;
 	HIPCHK(e);
-	d->graph[which] = g;
-	HIPCHK(hipGraphInstantiate(&d->exec[which], g, nullptr, nullptr, 0));
+	d->graph[v][which] = g;
+	HIPCHK(hipGraphInstantiate(&d->exec[v][which], g, nullptr, nullptr, 0));
 	return YALM_OK;
+}
+
+// Both attention + Wo forms of graph `which` (captured before any replay is queued).
+static int ensure_graphs(yalm_decoder_s *d, int which) {
+	const bool now = d->awo_local_now;
+	d->awo_local_now = false;
+	int r = ensure_graph(d, which);
+	if (r == YALM_OK && d->attn_wo && d->awo_local_max > 0) {
+		d->awo_local_now = true;
+		r = ensure_graph(d, which);
+	}
+	d->awo_local_now = now;
+	return r;
 }
 
 static int validate_config(const yalm_config *c) {
@@ -831,11 +873,13 @@ static int validate_config(const yalm_config *c) {
 }
 
 static void destroy_decoder(yalm_decoder_s *d) {
-	for (int i = 0; i < N_GRAPHS; ++i) {
-		if (d->exec[i])
-			(void)hipGraphExecDestroy(d->exec[i]);
-		if (d->graph[i])
-			(void)hipGraphDestroy(d->graph[i]);
+	for (int v = 0; v < 2; ++v) {
+		for (int i = 0; i < N_GRAPHS; ++i) {
+			if (d->exec[v][i])
+				(void)hipGraphExecDestroy(d->exec[v][i]);
+			if (d->graph[v][i])
+				(void)hipGraphDestroy(d->graph[v][i]);
+		}
 	}
 	if (d->comm)
 		(void)ncclCommDestroy((ncclComm_t)d->comm);
@@ -864,7 +908,7 @@ int dalloc(yalm_decoder_s *d, void **p, size_t bytes) {
 static int replay(yalm_decoder_s *d, int which) {
 	if (d->eager)
 		return enqueue_forward(d, which);
-	HIPCHK(hipGraphLaunch(d->exec[which], d->stream));
+	HIPCHK(hipGraphLaunch(d->exec[d->awo_local_now ? 1 : 0][which], d->stream));
 	if (d->graph_sync)
 		HIPCHK(hipStreamSynchronize(d->stream));
 	return YALM_OK;
@@ -1103,10 +1147,12 @@ extern "C" int yalm_forward(yalm_decoder d, int token, int pos, int mode, float 
 	ARGCHK(token >= 0 && token < d->vocab_full, "token out of range");
 	ARGCHK(pos >= 0, "negative pos");
 	const int which = mode == YALM_HYDRATE_KV_CACHE ? GRAPH_HYDRATE : GRAPH_LOGITS;
+	d->awo_local_now = use_local_at(d, pos);
 	TRY(ensure_graph(d, which));
 	set_step_kernel<<<1, 1, 0, d->stream>>>(d->step, token, pos, 0);
 	HIPCHK(hipGetLastError());
 	TRY(replay(d, which));
+	d->host_pos = pos; // OUTPUT / HYDRATE forwards do not advance the device position
 	if (which == GRAPH_LOGITS) {
 		HIPCHK(hipStreamSynchronize(d->stream));
 		TRY(engine_check(d));
@@ -1118,16 +1164,20 @@ extern "C" int yalm_forward(yalm_decoder d, int token, int pos, int mode, float 
 
 extern "C" int yalm_enqueue_greedy(yalm_decoder d, int n_steps) {
 	ARGCHK(d, "null decoder");
-	TRY(ensure_graph(d, GRAPH_GREEDY));
-	for (int i = 0; i < n_steps; ++i)
+	TRY(ensure_graphs(d, GRAPH_GREEDY));
+	for (int i = 0; i < n_steps; ++i) { // each replay advances the device position by one
+		d->awo_local_now = use_local_at(d, d->host_pos);
 		TRY(replay(d, GRAPH_GREEDY));
+		if (d->host_pos >= 0)
+			++d->host_pos;
+	}
 	return YALM_OK;
 }
 
 extern "C" int yalm_generate_greedy(yalm_decoder d, int token, int pos, int n_steps, int *out_tokens) {
 	ARGCHK(d && out_tokens, "null argument");
 	ARGCHK(token >= 0 && token < d->vocab_full && pos >= 0 && n_steps >= 0, "bad token/pos/n_steps");
-	TRY(ensure_graph(d, GRAPH_GREEDY));
+	TRY(ensure_graphs(d, GRAPH_GREEDY));
 	int done = 0;
 	bool first = true;
 	while (done < n_steps) {
@@ -1138,8 +1188,11 @@ extern "C" int yalm_generate_greedy(yalm_decoder d, int token, int pos, int n_st
 			set_step_kernel<<<1, 1, 0, d->stream>>>(d->step, out_tokens[done - 1], pos + done, 1);
 		HIPCHK(hipGetLastError());
 		first = false;
-		for (int i = 0; i < batch; ++i)
+		for (int i = 0; i < batch; ++i) {
+			d->awo_local_now = use_local_at(d, (long long)pos + done + i);
 			TRY(replay(d, GRAPH_GREEDY));
+		}
+		d->host_pos = (long long)pos + done + batch;
 		HIPCHK(hipMemcpyAsync(out_tokens + done, d->tokens, sizeof(int) * batch, hipMemcpyDeviceToHost, d->stream));
 		HIPCHK(hipStreamSynchronize(d->stream));
 		TRY(engine_check(d));
@@ -1167,6 +1220,7 @@ extern "C" int yalm_block(yalm_decoder d, int layer, int pos, int kv_sink, int k
 	       "bad kv indices");
 	set_step_full_kernel<<<1, 1, 0, d->stream>>>(d->step, pos, kv_sink, kv_pos, kv_len);
 	HIPCHK(hipGetLastError());
+	d->awo_local_now = d->attn_wo && kv_len <= d->awo_local_max;
 	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_layer_t, d, layer));
 	HIPCHK(hipStreamSynchronize(d->stream));
 	return YALM_OK;
@@ -1248,6 +1302,16 @@ static int enqueue_one_t(yalm_decoder_s *d, int kernel_id, int l) {
 		if constexpr (WT::BYTES <= 2)
 			return launch_ffn<WT>(d, w, l);
 		break;
+	case 8: // fused attention + Wo: granule hand-off form / short-context form
+	case 9:
+		if constexpr (WT::BYTES <= 2) {
+			const bool now = d->awo_local_now;
+			d->awo_local_now = kernel_id == 9;
+			const int r = launch_attn_wo<WT>(d, w, l);
+			d->awo_local_now = now;
+			return r;
+		}
+		break;
 	}
 	set_err("bad kernel_id");
 	return YALM_ERR_ARG;
@@ -1291,7 +1355,9 @@ extern "C" int yalm_attn_wo_trace(yalm_decoder d, unsigned long long *host, size
 }
 
 extern "C" int yalm_time_kernel(yalm_decoder d, int kernel_id, int iters, float *avg_ms) {
-	ARGCHK(d && avg_ms && iters > 0 && kernel_id >= 0 && kernel_id <= 7, "bad argument");
+	ARGCHK(d && avg_ms && iters > 0 && kernel_id >= 0 && kernel_id <= 9, "bad argument");
+	ARGCHK(kernel_id < 8 || d->attn_wo, "kernels 8/9 (fused attention + Wo) need yalm_decoder_attn_wo");
+	ARGCHK(kernel_id != 9 || d->awo_local_max > 0, "kernel 9 (short-context attention + Wo) is disabled");
 	ARGCHK(kernel_id != 6 || d->engine, "kernel 6 (engine) needs a decoder running the persistent engine");
 	ARGCHK(kernel_id != 7 || d->ffn, "kernel 7 (fused feed-forward) needs a decoder with yalm_decoder_ffn");
 	hipEvent_t e0, e1;
@@ -1336,13 +1402,15 @@ extern "C" int yalm_set_gemv_config(yalm_decoder d, int kind, int threads, int u
 	d->gemv[kind] = GemvCfg{threads, unroll, gpw};
 	// captured graphs bake the old geometry: drop them
 	HIPCHK(hipStreamSynchronize(d->stream));
-	for (int i = 0; i < N_GRAPHS; ++i) {
-		if (d->exec[i])
-			(void)hipGraphExecDestroy(d->exec[i]);
-		if (d->graph[i])
-			(void)hipGraphDestroy(d->graph[i]);
-		d->exec[i] = nullptr;
-		d->graph[i] = nullptr;
+	for (int v = 0; v < 2; ++v) {
+		for (int i = 0; i < N_GRAPHS; ++i) {
+			if (d->exec[v][i])
+				(void)hipGraphExecDestroy(d->exec[v][i]);
+			if (d->graph[v][i])
+				(void)hipGraphDestroy(d->graph[v][i]);
+			d->exec[v][i] = nullptr;
+			d->graph[v][i] = nullptr;
+		}
 	}
 	return YALM_OK;
 }
@@ -1376,6 +1444,12 @@ extern "C" const char *yalm_kernel_name(yalm_decoder d, int kernel_id) {
 		break;
 	case 7:
 		s = std::string("ffn_kernel<") + wt + ", ";
+		break;
+	case 8:
+		s = std::string("attn_wo_kernel<") + wt + ", ";
+		break;
+	case 9:
+		s = std::string("attn_wo_local_kernel<") + wt + ", ";
 		break;
 	default:
 		s = "";

@@ -109,6 +109,7 @@ _sig("yalm_decoder_attn_wo", c_int, [c_void_p])
 _sig("yalm_decoder_ffn", c_int, [c_void_p])
 _sig("yalm_ffn_trace", c_int, [c_void_p, c_void_p, ctypes.c_size_t, ctypes.POINTER(c_int)])
 _sig("yalm_attn_wo_trace", c_int, [c_void_p, c_void_p, ctypes.c_size_t, ctypes.POINTER(c_int), ctypes.POINTER(c_int)])
+_sig("yalm_attn_wo_local_trace", c_int, [c_void_p, c_void_p, ctypes.c_size_t, ctypes.POINTER(c_int)])
 _sig("yalm_engine_trace", c_int, [c_void_p, c_void_p, ctypes.c_size_t, ctypes.POINTER(c_int)])
 _sig("yalm_matmul", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int])
 _sig("yalm_mha", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int])
@@ -131,7 +132,7 @@ EXPORTED = [
     "yalm_time_kernel", "yalm_kernel_name", "yalm_set_gemv_config", "yalm_matmul", "yalm_mha", "yalm_ffn",
     "yalm_prefill", "yalm_prefill_time", "yalm_gemm_f16", "yalm_attn_prefill", "yalm_tp_unique_id",
     "yalm_decoder_create_tp", "yalm_copy_2d", "yalm_tp_ipc_alloc", "yalm_decoder_create_tp_ipc",
-    "yalm_decoder_engine", "yalm_engine_trace", "yalm_decoder_attn_wo", "yalm_attn_wo_trace",
+    "yalm_decoder_engine", "yalm_engine_trace", "yalm_decoder_attn_wo", "yalm_attn_wo_trace", "yalm_attn_wo_local_trace",
     "yalm_decoder_ffn", "yalm_ffn_trace",
 ]
 
@@ -440,6 +441,14 @@ class Decoder:
         nb, na = c_int(), c_int()
         check(lib.yalm_attn_wo_trace(self.h, buf.ctypes.data, buf.size, ctypes.byref(nb), ctypes.byref(na)))
         return buf[: 4 * nb.value].reshape(nb.value, 4), na.value
+
+    def attn_wo_local_trace(self) -> np.ndarray:
+        """(workgroups, 4) uint64 stamps of the last short-context attention + Wo
+        launch (attn_wo_local_kernel; decoder created with YALM_ATTN_WO_TRACE=1)."""
+        buf = np.zeros(4 * 8192, np.uint64)
+        nb = c_int()
+        check(lib.yalm_attn_wo_local_trace(self.h, buf.ctypes.data, buf.size, ctypes.byref(nb)))
+        return buf[: 4 * nb.value].reshape(nb.value, 4)
 
     @property
     def ffn(self) -> bool:
