@@ -39,6 +39,28 @@ def test_gemm_exact_integers(M_, N, K):
     np.testing.assert_array_equal(c, ref.astype(np.float32))
 
 
+# GEMM forms (yalm_amd/csrc/prefill.h gemm_nt_kernel): LDS-DMA stages 2 / 3 and the
+# 128 x 256 ("wide") tile; read per launch from the environment
+FORMS = {"s3-auto": {}, "s2": {"YALM_PF_STAGES": "2"}, "s3-wide": {"YALM_PF_WIDE": "1"},
+         "s2-wide": {"YALM_PF_STAGES": "2", "YALM_PF_WIDE": "1"}, "s3-narrow": {"YALM_PF_WIDE": "0"}}
+
+
+@pytest.mark.parametrize("form", list(FORMS))
+@pytest.mark.parametrize("M_,N,K", [(200, 256, 192), (37, 768, 128), (1, 256, 64), (513, 5120, 640)])
+def test_gemm_forms_exact(form, M_, N, K, monkeypatch):
+    """Every stage count / tile form is exact on f16-exact integer data (any
+    staging race or fragment-map error shows as a wrong integer); K tiles 1..10."""
+    for k, v in FORMS[form].items():
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(M_ + N + K)
+    a = rng.integers(-4, 5, size=(M_, K)).astype(np.float16)
+    w = rng.integers(-4, 5, size=(N, K)).astype(np.float16)
+    w[:, 0] += np.arange(N, dtype=np.float16) % 7
+    c = rt().gemm_f16(a, w)
+    ref = a.astype(np.int64) @ w.astype(np.int64).T
+    np.testing.assert_array_equal(c, ref.astype(np.float32))
+
+
 @pytest.mark.parametrize("M_,N,K", [(300, 384, 512), (4096, 128, 3072)])
 def test_gemm_random(M_, N, K):
     rng = np.random.default_rng(7)
@@ -92,6 +114,27 @@ CFGS = {
     "gqa-d128": M.ModelConfig(dim=512, hidden_dim=1024, head_dim=128, n_layers=3, n_heads=4, n_kv_heads=2,
                               vocab_size=1024, max_seq_len=320, rope_theta=1e6, act=M.SILU, weight_dtype=M.F16),
 }
+
+
+@pytest.mark.parametrize("form", ["s3-auto", "s2", "s3-wide"])
+def test_prefill_forms_match_decode(form, monkeypatch):
+    """The whole prefill in each GEMM form (the wide tile on every GEMM with N %
+    256 == 0, incl. the vocab-tiled logits epilogue run once per column half)."""
+    for k, v in FORMS[form].items():
+        monkeypatch.setenv(k, v)
+    cfg = CFGS["gqa-d128"]
+    R = rt()
+    dm = R.DeviceModel.synthetic(cfg, seed=4)
+    tokens = np.random.default_rng(5).integers(0, cfg.vocab_size, size=90).astype(np.int32)
+    dec_p = R.Decoder(dm)
+    dec_d = R.Decoder(dm)
+    try:
+        err = np.max(np.abs(dec_p.prefill(tokens)[:89] - _decode_logprobs(dec_d, tokens)))
+        assert err <= LP_ATOL, (form, err)
+    finally:
+        dec_p.close()
+        dec_d.close()
+        dm.close()
 
 
 @pytest.mark.parametrize("name", list(CFGS))

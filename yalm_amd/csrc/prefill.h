@@ -249,10 +249,35 @@ struct BSrc {
 };
 
 // C[M, N] (epilogue) = A[M, K] · W_b[N, K]^T for b < NB (NB = 2: W1 and W3
-// share the A tile). N % 128 == 0, K % 64 == 0, any M. Two LDS buffers; the
-// next K tile's LDS-DMA is issued before the current tile's MFMAs (the
-// 2-phase structure of cdna_hip_programming.md §5.5 T3+T4, minimum form).
-template <class EPI, int NB>
+// share the A tile). N % 128 == 0, K % 64 == 0, any M.
+//   NS = 2: two LDS buffers; the next K tile's LDS-DMA is issued before the
+//     current tile's MFMAs and drained (vmcnt(0) + barrier) after them (the
+//     2-phase structure of cdna_hip_programming.md §5.5 T3+T4, minimum form).
+//   NS = 3: three LDS buffers, ONE tile kept in flight across every barrier
+//     (cdna_hip_programming.md §5 "Pipelining across barriers": counted
+//     vmcnt(N) — N = this thread's LDS-DMA instructions per tile — and a raw
+//     s_barrier with lgkmcnt(0) only; __syncthreads() would drain the DMA).
+//     Per K step: wait for tile kt (tile kt + 1 may stay in flight) -> barrier
+//     (every wave's tile kt landed; every wave done reading tile kt - 1) ->
+//     issue tile kt + 2 into tile kt - 1's buffer -> MFMAs on tile kt.
+template <int NB>
+constexpr int gemm_lds_per_tile() {
+	return (1 + NB) * BM / 8 / (THREADS / 64); // LDS-DMA instructions per thread per K tile
+}
+__device__ __forceinline__ void raw_barrier() {
+	asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+template <int N>
+__device__ __forceinline__ void vmcnt_wait() {
+	asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// WIDE: a 128 x 256 output tile for a single weight matrix, run as NB = 2 with
+// the two B tiles = columns [col0, col0 + 128) and [col0 + 128, col0 + 256) of
+// the same B: twice the MFMAs per A fragment read from LDS (the GLU kernel's
+// shape, ~1 PF/s where the 128 x 128 tile reached 0.55-0.75); the narrow
+// epilogue runs once per column half.
+template <class EPI, int NB, int NS, bool WIDE = false>
 __global__ __launch_bounds__(THREADS) void gemm_nt_kernel(const uint16_t *__restrict__ A, int M, int K, BSrc B0,
                                                           BSrc B1, int N, EPI epi) {
 	extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
@@ -264,7 +289,9 @@ __global__ __launch_bounds__(THREADS) void gemm_nt_kernel(const uint16_t *__rest
 
 	// tile index: XCD-aware (blocks b, b+8, ... share an XCD's L2): consecutive
 	// tiles of one XCD walk down M for a fixed N panel (the W panel is reused)
-	const int tiles_m = (M + BM - 1) / BM, tiles_n = N / BN;
+	static_assert(!WIDE || NB == 2, "the wide tile runs as two B tiles");
+	constexpr int TBN = WIDE ? 2 * BN : BN; // output columns per tile
+	const int tiles_m = (M + BM - 1) / BM, tiles_n = N / TBN;
 	const int nwg = tiles_m * tiles_n;
 	int wg = blockIdx.x;
 	{
@@ -272,7 +299,7 @@ __global__ __launch_bounds__(THREADS) void gemm_nt_kernel(const uint16_t *__rest
 		wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
 	}
 	const int tm = wg % tiles_m, tn = wg / tiles_m;
-	const int row0 = tm * BM, col0 = tn * BN;
+	const int row0 = tm * BM, col0 = tn * TBN;
 
 	f32x16_t acc[NB][2][2];
 #pragma unroll
@@ -288,7 +315,7 @@ __global__ __launch_bounds__(THREADS) void gemm_nt_kernel(const uint16_t *__rest
 	int w0r, w0n, w1r = 0, w1n = 1;
 	B0.tile(col0, w0, w0r, w0n);
 	if constexpr (NB == 2)
-		B1.tile(col0, w1, w1r, w1n);
+		B1.tile(WIDE ? col0 + BN : col0, w1, w1r, w1n);
 	auto stage = [&](int buf, int kt) {
 		uint16_t *base = smem + buf * BUF;
 		stage_tile(base, A, K, row0, M, kt * BK, wave, lane);
@@ -296,14 +323,7 @@ __global__ __launch_bounds__(THREADS) void gemm_nt_kernel(const uint16_t *__rest
 		if constexpr (NB == 2)
 			stage_tile(base + 2 * TILE, w1, K, w1r, w1n, kt * BK, wave, lane);
 	};
-	stage(0, 0);
-	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-	__syncthreads();
-	int cur = 0;
-	for (int kt = 0; kt < nk; ++kt) {
-		if (kt + 1 < nk)
-			stage(cur ^ 1, kt + 1);
-		const uint16_t *a_t = smem + cur * BUF;
+	auto compute = [&](const uint16_t *a_t) {
 #pragma unroll
 		for (int s = 0; s < BK / 16; ++s) {
 			half8_t af[2], bf[NB][2];
@@ -323,14 +343,51 @@ __global__ __launch_bounds__(THREADS) void gemm_nt_kernel(const uint16_t *__rest
 					for (int j = 0; j < 2; ++j)
 						acc[b][i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[b][j], acc[b][i][j], 0, 0, 0);
 		}
+	};
+	if constexpr (NS == 2) {
+		stage(0, 0);
 		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 		__syncthreads();
-		cur ^= 1;
+		int cur = 0;
+		for (int kt = 0; kt < nk; ++kt) {
+			if (kt + 1 < nk)
+				stage(cur ^ 1, kt + 1);
+			compute(smem + cur * BUF);
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			__syncthreads();
+			cur ^= 1;
+		}
+	} else {
+		constexpr int L = gemm_lds_per_tile<NB>();
+		stage(0, 0);
+		if (nk > 1)
+			stage(1, 1);
+		int cur = 0; // buffer of tile kt
+		for (int kt = 0; kt < nk; ++kt) {
+			if (kt + 1 < nk)
+				vmcnt_wait<L>(); // tile kt landed (this thread's DMAs); tile kt + 1 may stay in flight
+			else
+				vmcnt_wait<0>();
+			raw_barrier();
+			if (kt + 2 < nk)
+				stage(cur == 0 ? 2 : cur - 1, kt + 2); // tile kt - 1's buffer: every wave is past reading it
+			compute(smem + cur * BUF);
+			cur = cur == 2 ? 0 : cur + 1;
+		}
+		raw_barrier(); // the epilogue may reuse the staging buffers (EpiLogits)
 	}
 	EPI e = epi;
 	if constexpr (EPI::NEEDS_LDS)
 		e.red = (float *)smem; // the staging buffers are free after the K loop's last barrier
-	e.template apply<NB>(acc, row0 + wm * 64, col0 + wn * 64, lane);
+	if constexpr (WIDE) {
+		typedef f32x16_t half_acc_t[1][2][2];
+		e.template apply<1>(*reinterpret_cast<half_acc_t *>(&acc[0]), row0 + wm * 64, col0 + wn * 64, lane);
+		if constexpr (EPI::NEEDS_LDS)
+			__syncthreads(); // the first half's readers are done with e.red
+		e.template apply<1>(*reinterpret_cast<half_acc_t *>(&acc[1]), row0 + wm * 64, col0 + BN + wn * 64, lane);
+	} else {
+		e.template apply<NB>(acc, row0 + wm * 64, col0 + wn * 64, lane);
+	}
 }
 
 // ---------------------------------------------------------------- attention

@@ -1,3 +1,4 @@
+#include <cstdlib>
 // prefill.hip — C ABI of the batched prefill / perplexity path (prefill.h):
 // yalm_prefill (prompt hydration + per-position log p(next), replacing the
 // reference's position-by-position loop in main.cpp:128-200 / 102-112) and
@@ -21,15 +22,39 @@ int pf_alloc(yalm_decoder_s *d, void **p, size_t bytes) {
 
 template <class EPI, int NB>
 int launch_gemm(const uint16_t *A, int M, int K, pf::BSrc b0, pf::BSrc b1, int N, const EPI &epi, hipStream_t st) {
-	auto kern = pf::gemm_nt_kernel<EPI, NB>;
-	const size_t lds = (size_t)2 * (1 + NB) * pf::TILE * sizeof(uint16_t);
-	static bool attr_set = false; // one per template instance
-	if (!attr_set) {
-		HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-		attr_set = true;
+	// LDS-DMA stages (YALM_PF_STAGES, 2 or 3; pf::gemm_nt_kernel)
+	// (both read per launch: tests switch them inside one process)
+	const int stages = getenv("YALM_PF_STAGES") && atoi(getenv("YALM_PF_STAGES")) == 2 ? 2 : 3;
+	// one weight matrix with N % 256 == 0 and N > 4096: the 128 x 256 tile. Measured on
+	// Llama-3.2-3B, T = 4096 (profiles/r2_prefill_kernels.txt): QKV (N 5120) 287 -> 276 us,
+	// logits (N 128256) 5.61 -> 4.74 ms; Wo / W2 (N 3072) 241 -> 269 us (half the
+	// workgroups: 1.5 rounds of 256 CUs), so narrower N keeps the 128 x 128 tile.
+	// YALM_PF_WIDE=0: never, 1: whenever N % 256 == 0.
+	const int wide_env = getenv("YALM_PF_WIDE") ? atoi(getenv("YALM_PF_WIDE")) : -1;
+	const bool wide = NB == 1 && wide_env != 0 && N % (2 * pf::BN) == 0 && (wide_env == 1 || N > 4096);
+	const void *kern = nullptr;
+	size_t lds;
+	if constexpr (NB == 1) {
+		if (wide) {
+			kern = stages == 3 ? (const void *)pf::gemm_nt_kernel<EPI, 2, 3, true>
+			                   : (const void *)pf::gemm_nt_kernel<EPI, 2, 2, true>;
+			b1 = b0;
+		}
 	}
-	const int nwg = ((M + pf::BM - 1) / pf::BM) * (N / pf::BN);
-	hipLaunchKernelGGL(kern, dim3(nwg), dim3(pf::THREADS), lds, st, A, M, K, b0, b1, N, epi);
+	if (wide) {
+		lds = (size_t)stages * 3 * pf::TILE * sizeof(uint16_t);
+	} else {
+		kern = stages == 3 ? (const void *)pf::gemm_nt_kernel<EPI, NB, 3> : (const void *)pf::gemm_nt_kernel<EPI, NB, 2>;
+		lds = (size_t)stages * (1 + NB) * pf::TILE * sizeof(uint16_t);
+	}
+	static bool attr_set[2][2] = {}; // per template instance, form and stage count
+	if (!attr_set[wide][stages - 2]) {
+		HIPCHK(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+		attr_set[wide][stages - 2] = true;
+	}
+	const int nwg = ((M + pf::BM - 1) / pf::BM) * (N / (wide ? 2 * pf::BN : pf::BN));
+	void *args[] = {(void *)&A, (void *)&M, (void *)&K, (void *)&b0, (void *)&b1, (void *)&N, (void *)&epi};
+	HIPCHK(hipLaunchKernel(kern, dim3(nwg), dim3(pf::THREADS), args, lds, st));
 	HIPCHK(hipGetLastError());
 	return YALM_OK;
 }
