@@ -41,8 +41,10 @@ def test_gemm_exact_integers(M_, N, K):
 
 # GEMM forms (yalm_amd/csrc/prefill.h gemm_nt_kernel): LDS-DMA stages 2 / 3 and the
 # 128 x 256 ("wide") tile; read per launch from the environment
-FORMS = {"s3-auto": {}, "s2": {"YALM_PF_STAGES": "2"}, "s3-wide": {"YALM_PF_WIDE": "1"},
-         "s2-wide": {"YALM_PF_STAGES": "2", "YALM_PF_WIDE": "1"}, "s3-narrow": {"YALM_PF_WIDE": "0"}}
+FORMS = {"auto": {}, "s2": {"YALM_PF_STAGES": "2"}, "s3": {"YALM_PF_STAGES": "3"},
+         "s3-wide": {"YALM_PF_STAGES": "3", "YALM_PF_WIDE": "1"},
+         "s2-wide": {"YALM_PF_STAGES": "2", "YALM_PF_WIDE": "1"},
+         "s3-narrow": {"YALM_PF_STAGES": "3", "YALM_PF_WIDE": "0"}}
 
 
 @pytest.mark.parametrize("form", list(FORMS))
@@ -116,7 +118,7 @@ CFGS = {
 }
 
 
-@pytest.mark.parametrize("form", ["s3-auto", "s2", "s3-wide"])
+@pytest.mark.parametrize("form", ["auto", "s3", "s2-wide"])
 def test_prefill_forms_match_decode(form, monkeypatch):
     """The whole prefill in each GEMM form (the wide tile on every GEMM with N %
     256 == 0, incl. the vocab-tiled logits epilogue run once per column half)."""

@@ -22,16 +22,19 @@ int pf_alloc(yalm_decoder_s *d, void **p, size_t bytes) {
 
 template <class EPI, int NB>
 int launch_gemm(const uint16_t *A, int M, int K, pf::BSrc b0, pf::BSrc b1, int N, const EPI &epi, hipStream_t st) {
-	// LDS-DMA stages (YALM_PF_STAGES, 2 or 3; pf::gemm_nt_kernel)
-	// (both read per launch: tests switch them inside one process)
-	const int stages = getenv("YALM_PF_STAGES") && atoi(getenv("YALM_PF_STAGES")) == 2 ? 2 : 3;
-	// one weight matrix with N % 256 == 0 and N > 4096: the 128 x 256 tile. Measured on
-	// Llama-3.2-3B, T = 4096 (profiles/r2_prefill_kernels.txt): QKV (N 5120) 287 -> 276 us,
-	// logits (N 128256) 5.61 -> 4.74 ms; Wo / W2 (N 3072) 241 -> 269 us (half the
-	// workgroups: 1.5 rounds of 256 CUs), so narrower N keeps the 128 x 128 tile.
-	// YALM_PF_WIDE=0: never, 1: whenever N % 256 == 0.
-	const int wide_env = getenv("YALM_PF_WIDE") ? atoi(getenv("YALM_PF_WIDE")) : -1;
-	const bool wide = NB == 1 && wide_env != 0 && N % (2 * pf::BN) == 0 && (wide_env == 1 || N > 4096);
+	// Form per GEMM, from per-kernel rocprofv3 times on Llama-3.2-3B at T = 4096
+	// (profiles/r2_prefill_kernels.txt): the two-matrix GLU GEMM keeps one K tile in
+	// flight across the barriers (3 LDS stages: 495 vs 633 us at 2); single-matrix
+	// GEMMs of moderate N keep the 128 x 128 tile with 2 stages (2 workgroups per CU:
+	// QKV 241 us vs 287 at 3 stages and 278 wide; Wo 154 vs 160; W2 equal); the vocab
+	// GEMM (N > 16384) takes the 128 x 256 tile with 3 stages (4.77 ms vs 5.27 / 5.61).
+	// YALM_PF_STAGES = 2 | 3 and YALM_PF_WIDE = 0 | 1 override (read per launch: tests
+	// switch them inside one process).
+	const char *se = getenv("YALM_PF_STAGES");
+	const char *we = getenv("YALM_PF_WIDE");
+	const bool big_n = N > 16384;
+	const bool wide = NB == 1 && N % (2 * pf::BN) == 0 && (we ? atoi(we) != 0 : big_n);
+	const int stages = se ? (atoi(se) == 2 ? 2 : 3) : (NB == 2 || wide ? 3 : 2);
 	const void *kern = nullptr;
 	size_t lds;
 	if constexpr (NB == 1) {
