@@ -218,8 +218,8 @@ static GemvCfg default_rb_cfg(int kind) {
 		switch (kind) {
 		case GK_W2:
 			return GemvCfg{512, 4, 1};
-		case GK_GLU:
-			return GemvCfg{1024, 2, 2};
+		case GK_GLU: // round-2 resweep (profiles/r2_sweep_rb_fp8.txt): 21.4 us vs 22.5 for {1024, 2, 2}
+			return GemvCfg{512, 2, 2};
 		default:
 			return GemvCfg{512, 2, 2};
 		}
@@ -951,6 +951,18 @@ static int create_decoder(const yalm_config *config, const yalm_model_weights *w
 	d->eager = getenv("YALM_EAGER") && atoi(getenv("YALM_EAGER")) != 0;
 	d->graph_sync = getenv("YALM_GRAPH_SYNC") && atoi(getenv("YALM_GRAPH_SYNC")) != 0;
 	d->ablate = getenv("YALM_ABLATE") ? atoi(getenv("YALM_ABLATE")) : 0;
+	// geometry overrides for A/B runs without a rebuild (same meaning as yalm_set_gemv_config):
+	// YALM_GEMV_CFG="kind:threads:unroll:gpw[,kind:threads:unroll:gpw...]", kind 0..4
+	if (const char *g = getenv("YALM_GEMV_CFG")) {
+		int k, t, u, w, n = 0;
+		for (const char *p = g; sscanf(p, "%d:%d:%d:%d%n", &k, &t, &u, &w, &n) == 4; p += n + (p[n] == ',')) {
+			if (k >= 0 && k < GK_N && (t == 0 || t == 256 || t == 512 || t == 1024) &&
+			    (u == 0 || u == 2 || u == 4 || u == 8) && w >= 0)
+				d->gemv[k] = GemvCfg{t, u, w};
+			if (!p[n])
+				break;
+		}
+	}
 	if ((r = dalloc(d, (void **)&d->step, sizeof(StepState))) || (r = dalloc(d, (void **)&d->x, sizeof(float) * c.dim)) ||
 	    (r = dalloc(d, (void **)&d->q, sizeof(float) * q_dim)) ||
 	    (r = dalloc(d, (void **)&d->xb2, sizeof(float) * q_dim)) ||
