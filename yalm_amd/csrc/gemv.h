@@ -187,6 +187,7 @@ struct PGlu {
 	int n;
 	float *out;
 	int n_groups;
+	int w3_rot = 0; // row-block kernel: stream each workgroup's W3 rows rotated by half its groups (rb_perm)
 	__device__ __forceinline__ void prologue() const {}
 	__device__ __forceinline__ const char *row(int g, int r) const {
 		return (r == 0 ? w1 : w3) + (size_t)g * n * WT::BYTES;
@@ -197,6 +198,20 @@ struct PGlu {
 	}
 	__device__ __forceinline__ void finish_all(int g, const float *acc) const { finish(g, acc, 0); }
 };
+
+// Row-block kernel item order: the local group a (group, row-of-group) item is
+// STREAMED for. Identity, except PGlu with w3_rot: a workgroup reads its W3 rows
+// rotated by half its groups, so the chip-wide W3 window sits hidden_dim / 2 rows
+// away from the W1 window instead of at the same offset of the other matrix
+// (the partials still land at the true (group, row), so results are unchanged).
+template <class P>
+__device__ __forceinline__ int rb_perm(const P &, int gl, int, int) {
+	return gl;
+}
+template <class WT, int ACT>
+__device__ __forceinline__ int rb_perm(const PGlu<WT, ACT> &p, int gl, int r, int ngl) {
+	return r == 1 && p.w3_rot ? (gl + (ngl >> 1)) % ngl : gl;
+}
 
 // Rotate the attention-sink keys by one position (infer.cpp:303-317,
 // infer.cu:679-697), executed by workgroup 0 of the QKV launch. Rows < kv_sink
@@ -568,7 +583,11 @@ __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__re
 	};
 	auto iaddr = [&](int vr, int c) {
 		const int gl = vr / R, r = vr - gl * R;
-		return p.row(b + gl * NB, r) + (size_t)c * CHB + lane_off;
+		return p.row(b + rb_perm(p, gl, r, ngl) * NB, r) + (size_t)c * CHB + lane_off;
+	};
+	auto pslot = [&](int vr) { // LDS partial slot of item row vr: its true (group, row)
+		const int gl = vr / R, r = vr - gl * R;
+		return (rb_perm(p, gl, r, ngl) * R + r) * W + wave;
 	};
 
 	int ivr = wave / nch, ic = wave - (wave / nch) * nch; // issue cursor
@@ -602,7 +621,7 @@ __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__re
 					if (cvr != cur) {
 						const float s = wave_sum(acc[0]);
 						if (lane == 0)
-							part[cur * W + wave] = s;
+							part[pslot(cur)] = s;
 						acc[0] = 0.0f;
 						cur = cvr;
 					}
@@ -616,7 +635,7 @@ __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__re
 		}
 		const float s = wave_sum(acc[0]);
 		if (lane == 0)
-			part[cur * W + wave] = s;
+			part[pslot(cur)] = s;
 	}
 	__syncthreads();
 	for (int gl = threadIdx.x; gl < ngl; gl += THREADS) {

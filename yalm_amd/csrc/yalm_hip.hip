@@ -699,6 +699,7 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 		p.n = c.dim;
 		p.out = d->hb;
 		p.n_groups = c.hidden_dim;
+		p.w3_rot = d->glu_w3_rot;
 		TRY((launch_gemv_d<WT, PGlu<WT, 1>, true>(d, p, d->x, w.rms_ffn, c.norm_eps, GK_GLU)));
 	} else {
 		PGlu<WT, 0> p;
@@ -707,6 +708,7 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 		p.n = c.dim;
 		p.out = d->hb;
 		p.n_groups = c.hidden_dim;
+		p.w3_rot = d->glu_w3_rot;
 		TRY((launch_gemv_d<WT, PGlu<WT, 0>, true>(d, p, d->x, w.rms_ffn, c.norm_eps, GK_GLU)));
 	}
 	if (!(ab & 16))
@@ -951,6 +953,7 @@ static int create_decoder(const yalm_config *config, const yalm_model_weights *w
 	d->eager = getenv("YALM_EAGER") && atoi(getenv("YALM_EAGER")) != 0;
 	d->graph_sync = getenv("YALM_GRAPH_SYNC") && atoi(getenv("YALM_GRAPH_SYNC")) != 0;
 	d->ablate = getenv("YALM_ABLATE") ? atoi(getenv("YALM_ABLATE")) : 0;
+	d->glu_w3_rot = getenv("YALM_GLU_W3_ROT") ? atoi(getenv("YALM_GLU_W3_ROT")) != 0 : 0;
 	// geometry overrides for A/B runs without a rebuild (same meaning as yalm_set_gemv_config):
 	// YALM_GEMV_CFG="kind:threads:unroll:gpw[,kind:threads:unroll:gpw...]", kind 0..4
 	if (const char *g = getenv("YALM_GEMV_CFG")) {
@@ -1303,6 +1306,7 @@ static int enqueue_one_t(yalm_decoder_s *d, int kernel_id, int l) {
 		p.n = c.dim;
 		p.out = d->hb;
 		p.n_groups = c.hidden_dim;
+		p.w3_rot = d->glu_w3_rot;
 		return launch_gemv_d<WT, PGlu<WT, 1>, true>(d, p, d->x, w.rms_ffn, c.norm_eps, GK_GLU);
 	}
 	case 1:
