@@ -96,6 +96,7 @@ struct yalm_decoder_s {
 	GemvCfg gemv[GK_N];
 	bool eager = false;     // YALM_EAGER=1: launch kernels directly (profilers that mis-handle graph replay)
 	bool graph_sync = false; // YALM_GRAPH_SYNC=1: synchronise after every replay
+	std::vector<void *> glu_il;      // YALM_GLU_INTERLEAVE=1: per layer [hidden][W1 row | W3 row] copies (device)
 	int glu_w3_rot = 0;      // YALM_GLU_W3_ROT=1: W1|W3 GEMV streams W3 rows rotated by half (gemv.h rb_perm)
 	int ablate = 0;          // YALM_ABLATE bitmask: skip qkv|attn|wo|glu|w2 (1|2|4|8|16), or (32) load no Wo
 	                         // weights in the fused attention + Wo launch; timing only, results wrong

@@ -188,8 +188,11 @@ struct PGlu {
 	float *out;
 	int n_groups;
 	int w3_rot = 0; // row-block kernel: stream each workgroup's W3 rows rotated by half its groups (rb_perm)
+	int il = 0;     // w1 = one [hidden][2][n] buffer: W1 row g, then W3 row g (decoder copy, YALM_GLU_INTERLEAVE)
 	__device__ __forceinline__ void prologue() const {}
 	__device__ __forceinline__ const char *row(int g, int r) const {
+		if (il)
+			return w1 + (size_t)(2 * g + r) * n * WT::BYTES;
 		return (r == 0 ? w1 : w3) + (size_t)g * n * WT::BYTES;
 	}
 	__device__ __forceinline__ void finish(int g, const float *acc, int lane) const {

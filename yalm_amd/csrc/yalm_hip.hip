@@ -700,6 +700,10 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 		p.out = d->hb;
 		p.n_groups = c.hidden_dim;
 		p.w3_rot = d->glu_w3_rot;
+		if (!d->glu_il.empty()) {
+			p.w1 = (const char *)d->glu_il[l];
+			p.il = 1;
+		}
 		TRY((launch_gemv_d<WT, PGlu<WT, 1>, true>(d, p, d->x, w.rms_ffn, c.norm_eps, GK_GLU)));
 	} else {
 		PGlu<WT, 0> p;
@@ -709,6 +713,10 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 		p.out = d->hb;
 		p.n_groups = c.hidden_dim;
 		p.w3_rot = d->glu_w3_rot;
+		if (!d->glu_il.empty()) {
+			p.w1 = (const char *)d->glu_il[l];
+			p.il = 1;
+		}
 		TRY((launch_gemv_d<WT, PGlu<WT, 0>, true>(d, p, d->x, w.rms_ffn, c.norm_eps, GK_GLU)));
 	}
 	if (!(ab & 16))
@@ -1004,6 +1012,24 @@ static int create_decoder(const yalm_config *config, const yalm_model_weights *w
 	}
 	if ((r = engine_init(d)) || (r = attn_wo_init(d)) || (r = ffn_init(d)))
 		return fail(r);
+	// opt-in: W1 and W3 interleaved row by row in one decoder-owned buffer per layer, so the
+	// W1|W3 GEMV streams ONE contiguous window (costs a copy of both matrices)
+	if (getenv("YALM_GLU_INTERLEAVE") && atoi(getenv("YALM_GLU_INTERLEAVE")) != 0 && !d->engine && !d->ffn &&
+	    c.weight_dtype != YALM_F32) {
+		const size_t rb = (size_t)c.dim * (c.weight_dtype == YALM_F16 ? 2 : 1);
+		for (int l = 0; l < c.n_layers; ++l) {
+			void *buf = nullptr;
+			if ((r = dalloc(d, &buf, 2 * rb * c.hidden_dim)))
+				return fail(r);
+			if (hipMemcpy2D(buf, 2 * rb, d->b[l].w1, rb, rb, c.hidden_dim, hipMemcpyDeviceToDevice) != hipSuccess ||
+			    hipMemcpy2D((char *)buf + rb, 2 * rb, d->b[l].w3, rb, rb, c.hidden_dim, hipMemcpyDeviceToDevice) !=
+			        hipSuccess) {
+				set_err("GLU interleave copy failed");
+				return fail(YALM_ERR_HIP);
+			}
+			d->glu_il.push_back(buf);
+		}
+	}
 	{ // work-stealing GEMV tail (gemv_dyn.h): single-GPU launch path, fp16 / fp8 weights.
 	  // Opt-in (YALM_DYN=1): measured slower on MI355X (Mistral-7B fp16: QKV 15.1 vs 12.0 us,
 	  // W1|W3 44.4 vs 39.6, W2 23.7 vs 20.8; static prefix alone 1-3 us slower)
@@ -1307,6 +1333,10 @@ static int enqueue_one_t(yalm_decoder_s *d, int kernel_id, int l) {
 		p.out = d->hb;
 		p.n_groups = c.hidden_dim;
 		p.w3_rot = d->glu_w3_rot;
+		if (!d->glu_il.empty()) {
+			p.w1 = (const char *)d->glu_il[l];
+			p.il = 1;
+		}
 		return launch_gemv_d<WT, PGlu<WT, 1>, true>(d, p, d->x, w.rms_ffn, c.norm_eps, GK_GLU);
 	}
 	case 1:
