@@ -57,6 +57,7 @@ struct AttnWoArgs {
 	                    // -1 = no weight loads (YALM_ABLATE bit 32, timing only: results wrong)
 	int delay;          // s_memrealtime ticks (10 ns) the Wo workgroups wait before their slice loads
 	                    // (YALM_ATTN_WO_DELAY, tuning knob: lets the attention chain start alone)
+	int spec;           // speculative gather once the slice has landed (YALM_AWO_SPEC)
 };
 
 // Eight 16-byte sc1 loads from arbitrary addresses in one statement, one vmcnt(0)
@@ -85,13 +86,45 @@ __device__ __forceinline__ void awo_ld8_sc1(u32x4_t (&v)[8], const void *const (
 // (deadline, s_memrealtime).
 template <int EPL, int XS>
 __device__ __forceinline__ bool awo_gather_gran(float (&xs)[XS][EPL], const unsigned long long *gran, int tid,
-                                                unsigned tag, unsigned long long deadline) {
+                                                unsigned tag, unsigned long long deadline, bool spec) {
 	constexpr int LPP = EPL / 2;   // 16-byte loads per piece
 	constexpr int NL = XS * LPP;   // 4, 8 or 16
 	constexpr int NB = (NL + 7) / 8;
 	constexpr int D = 128;
 	constexpr int HPP = 64 * EPL / D; // heads per piece (4 or 8)
 	bool alive = true;
+	// speculative gather (spec, single-batch shapes): issued only once this wave's Wo slice
+	// has landed (a load samples memory when it is ISSUED; issued earlier it would read
+	// stale tags), by which time the heads are usually written: when every tag matches,
+	// the sentinel poll and its extra round trip are skipped; otherwise fall through
+	if (spec && NB == 1) {
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		const void *a[8];
+#pragma unroll
+		for (int i = 0; i < 8; ++i) {
+			const int l = i < NL ? i : 0;
+			const int k = l / LPP, e = (l % LPP) * 2;
+			a[i] = gran + (size_t)(k * ATTN_THREADS + tid) * EPL + e;
+		}
+		u32x4_t v[8];
+		awo_ld8_sc1(v, a);
+		bool ok = true;
+#pragma unroll
+		for (int i = 0; i < 8; ++i)
+			ok = ok && v[i][1] == tag && v[i][3] == tag;
+		if (__all(ok)) {
+#pragma unroll
+			for (int i = 0; i < 8; ++i) {
+				if (i < NL) {
+					const int k = i / LPP, e = (i % LPP) * 2;
+					const uint32_t w0 = v[i][0], w1 = v[i][2];
+					xs[k][e] = __uint_as_float(w0);
+					xs[k][e + 1] = __uint_as_float(w1);
+				}
+			}
+			return true;
+		}
+	}
 	// cheap wait first: one lane per covered head polls that head's last granule
 	// (one 8-byte sc1 load per lane), so the full re-reads below run ~once
 	{
@@ -214,7 +247,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 	// only for the heads its columns cover), then dot them into every resident row.
 	const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 	float xs[XS][EPL];
-	if (!awo_gather_gran<EPL, XS>(xs, p.gran, tid, epoch, t0 + AWO_TIMEOUT) && lane == 0)
+	if (!awo_gather_gran<EPL, XS>(xs, p.gran, tid, epoch, t0 + AWO_TIMEOUT, p.spec != 0) && lane == 0)
 		__hip_atomic_fetch_or(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 	if (tr)
 		tr[2] = __builtin_amdgcn_s_memrealtime();

@@ -139,7 +139,8 @@ struct yalm_decoder_s {
 	int awo_S = 0;                   // key-chunk splits per kv head
 	unsigned long long *awo_trace = nullptr; // YALM_ATTN_WO_TRACE=1: [grid][4] stamps of the last launch
 	int awo_win = 0;                 // Wo loads in flight per lane (YALM_ATTN_WO_WIN), -1 = none (ablation)
-	int awo_delay = 0;               // ticks the Wo workgroups wait before their slice loads (YALM_ATTN_WO_DELAY)
+	int awo_delay = 0;
+	int awo_spec = 0;                // YALM_AWO_SPEC=1: speculative gather after the slice landed (attn_wo.h)               // ticks the Wo workgroups wait before their slice loads (YALM_ATTN_WO_DELAY)
 	unsigned long long *awo_gran = nullptr; // [n_layers][q_dim] attention outputs as {value, epoch} granules
 	unsigned *awo_err = nullptr;     // error word (bounded spins that gave up)
 	int awo_local_max = 0;           // kv_len up to which the short-context kernel runs (YALM_AWO_LOCAL, 0 = never)

@@ -432,6 +432,8 @@ static int attn_wo_init(yalm_decoder_s *d) {
 	// stream (tools/sweep_awo.sh, profiles/r2_sweep_awo_delay.txt: 10.6 -> 10.1 us at kv_len 17,
 	// 10.6 -> 10.4 at kv_len 151; 0.4-0.6 us delays lose it again at long contexts)
 	d->awo_delay = denv ? std::max(0, atoi(denv)) : 20;
+	const char *spenv = getenv("YALM_AWO_SPEC");
+	d->awo_spec = spenv ? atoi(spenv) != 0 : 0;
 	const char *tenv = getenv("YALM_ATTN_WO_TRACE");
 	if (tenv && atoi(tenv) != 0)
 		TRY(dalloc(d, (void **)&d->awo_trace, sizeof(unsigned long long) * 4 * d->awo_nb));
@@ -491,6 +493,7 @@ static int launch_attn_wo(yalm_decoder_s *d, const yalm_block_weights &w, int la
 	p.trace = d->awo_trace;
 	p.win = d->awo_win;
 	p.delay = d->awo_delay;
+	p.spec = d->awo_spec;
 	const int G = c.n_heads / c.n_kv_heads;
 	if constexpr (WT::BYTES == 2 || WT::BYTES == 1) {
 		if (p.q_dim * WT::BYTES == 4096)
