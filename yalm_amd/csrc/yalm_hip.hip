@@ -433,7 +433,7 @@ static int attn_wo_init(yalm_decoder_s *d) {
 	// 10.6 -> 10.4 at kv_len 151; 0.4-0.6 us delays lose it again at long contexts)
 	d->awo_delay = denv ? std::max(0, atoi(denv)) : 20;
 	const char *spenv = getenv("YALM_AWO_SPEC");
-	d->awo_spec = spenv ? atoi(spenv) != 0 : 0;
+	d->awo_spec = spenv ? atoi(spenv) != 0 : 1; // profiles/r2c_ab_awo_spec.txt: 10.17 -> 9.76 us (kv 17)
 	const char *tenv = getenv("YALM_ATTN_WO_TRACE");
 	if (tenv && atoi(tenv) != 0)
 		TRY(dalloc(d, (void **)&d->awo_trace, sizeof(unsigned long long) * 4 * d->awo_nb));
