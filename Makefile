@@ -4,7 +4,7 @@ CXX ?= g++
 ARCH ?= gfx950
 HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall
 CSRC = yalm_amd/csrc
-HIP_SRCS = $(CSRC)/yalm_hip.hip $(CSRC)/prefill.hip $(CSRC)/engine.hip $(CSRC)/dyn.hip $(CSRC)/awl.hip
+HIP_SRCS = $(CSRC)/yalm_hip.hip $(CSRC)/prefill.hip
 HIP_OBJS = $(patsubst $(CSRC)/%.hip,build/%.o,$(HIP_SRCS))
 HIP_HDRS = $(wildcard $(CSRC)/*.h) include/yalm_hip.h
 
@@ -13,9 +13,6 @@ all: yalm_amd/libyalm_hip.so oracle host
 yalm_amd/libyalm_hip.so: $(HIP_OBJS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(HIP_OBJS) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
-# the work-stealing GEMV keeps several dequeues in flight: the atomic optimizer
-# would turn each into a wave-aggregated atomic whose result is waited at once
-build/dyn.o: HIPFLAGS += -mllvm -amdgpu-atomic-optimizer-strategy=None
 
 build/%.o: $(CSRC)/%.hip $(HIP_HDRS)
 	@mkdir -p build

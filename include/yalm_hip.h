@@ -133,40 +133,28 @@ int yalm_get_x(yalm_decoder d, float *host);
 int yalm_set_x(yalm_decoder d, const float *host);
 int yalm_get_logits(yalm_decoder d, float *host);
 /* Average device time (ms) of one kernel of the forward, launched eagerly on
- * the decoder's stream `iters` times between HIP events. kernel_id: 0 = QKV
- * GEMV, 1 = attention, 2 = Wo GEMV, 3 = W1/W3 GEMV+GLU, 4 = W2 GEMV,
- * 5 = logits GEMV, 6 = the whole-token engine launch (greedy mode; advances
- * the decoder's device step), 7 = the fused feed-forward launch (rmsnorm + W1/W3
- * + GLU + W2 + residual, yalm_decoder_ffn), 8 / 9 = the fused attention + Wo
- * launch in its granule hand-off / short-context form (yalm_decoder_attn_wo).
- * Used by bench.py for the roofline of the dominant kernel. */
+ * the decoder's stream `iters` times between HIP events (layers rotated so the
+ * weights come from HBM). kernel_id: 0 = QKV GEMV, 1 = attention, 2 = Wo GEMV,
+ * 3 = W1/W3 GEMV+GLU, 4 = W2 GEMV, 5 = logits GEMV, 8 = the fused attention + Wo
+ * launch (yalm_decoder_attn_wo; each timed launch gets a fresh step epoch, so its
+ * Wo waves wait for the heads as in a real forward; the epoch-bump launches are
+ * timed separately and subtracted). Used by bench.py for the roofline of the
+ * dominant kernel. */
 int yalm_time_kernel(yalm_decoder d, int kernel_id, int iters, float *avg_ms);
 /* Override the GEMV launch geometry of one weight-streaming kernel kind
  * (0 = QKV, 1 = Wo, 2 = W1/W3, 3 = W2, 4 = logits): workgroup size
  * 256|512|1024, unroll (16-byte loads in flight per lane) 2|4|8, and `gpw` =
- * workgroups per CU of the row-block kernel (row groups per wave of the legacy
- * kernel under YALM_GEMV_LEGACY=1); 0 = automatic.
+ * workgroups per CU of the row-block kernel; 0 = automatic.
  * Drops captured graphs (re-captured on next use). Tuning/ablation hook. */
 int yalm_set_gemv_config(yalm_decoder d, int kind, int threads, int unroll, int gpw);
-/* Name of kernel_id's device function (to match rocprofv3 summaries).
- * kernel_id 6 = the persistent per-token engine (yalm_decoder_engine). */
+/* Name of kernel_id's device function (to match rocprofv3 summaries). */
 const char *yalm_kernel_name(yalm_decoder d, int kernel_id);
-/* 1 if this decoder runs each token as ONE persistent launch (engine.h: LDS-DMA
- * weight ring + in-launch epoch seams), 0 if it uses the per-kernel launch path
- * (tensor parallel, unsupported shapes, or YALM_ENGINE unset/0 at creation: the
- * engine is opt-in, YALM_ENGINE=1).
- * yalm_time_kernel(d, 6, ...) times one greedy engine launch. */
-int yalm_decoder_engine(yalm_decoder d);
 /* 1 if this decoder's launch path runs attention and the Wo projection (+ the
  * residual add) as ONE launch (attn_wo.h: the Wo weight stream overlaps the
  * attention; replaces attn + fused_matmul_add_residuals, infer.cu:338-524, 270):
  * single GPU, head_dim 128, fp16 / fp8 weights with 4 or 8 KB Wo rows, and
- * YALM_ATTN_WO not 0 at creation. 0 = two separate launches.
- * Two forms, picked per token from the position the host tracks (both correct
- * at any kv_len): while kv_len <= YALM_AWO_LOCAL (opt-in, default 0 = never) every
- * Wo workgroup recomputes the attention from the L2-resident KV cache
- * (attn_wo_local_kernel, no cross-CU hand-off); longer contexts hand the split-KV
- * attention output to the Wo workgroups as {value, epoch} granules. */
+ * YALM_ATTN_WO not 0 at creation. 0 = two separate launches. The split-KV
+ * attention output is handed to the Wo workgroups as {value, epoch} granules. */
 int yalm_decoder_attn_wo(yalm_decoder d);
 /* Timeline of the most recent fused attention + Wo launch (decoder created with
  * YALM_ATTN_WO_TRACE=1): 4 s_memrealtime (100 MHz) stamps per workgroup at
@@ -175,33 +163,6 @@ int yalm_decoder_attn_wo(yalm_decoder d);
  * [0, *attention_workgroups) are attention, the rest Wo. */
 int yalm_attn_wo_trace(yalm_decoder d, unsigned long long *host, size_t count, int *workgroups,
                        int *attention_workgroups);
-/* The same for the short-context form (attn_wo_local_kernel, one workgroup per 16
- * Wo rows): start, attention output in LDS, Wo slice landed (the trace waits for
- * it), end. */
-int yalm_attn_wo_local_trace(yalm_decoder d, unsigned long long *host, size_t count, int *workgroups);
-/* 1 if this decoder's launch path runs the whole feed-forward half of a block
- * (rmsnorm, W1/W3 + SiLU/GELU-GLU, W2 + residual; infer.cu:598-620 + 270-288,
- * which the reference launches as three kernels) as ONE launch (ffn.h: the W2
- * weight stream is in flight while the last GLU rows finish; the hb hand-off is
- * an in-launch seam over all workgroups, one per CU): single GPU, fp16 / fp8
- * weights, dim and hidden_dim multiples of 512 (fp16) / 1024 (fp8) elements,
- * and YALM_FFN=1 at creation (opt-in: slower than the separate launches on
- * MI355X). 0 = separate GLU and W2 launches. */
-int yalm_decoder_ffn(yalm_decoder d);
-/* Timeline of the most recent fused feed-forward launch (decoder created with
- * YALM_FFN_TRACE=1): 8 words per workgroup at [w * 8 + k]: s_memrealtime
- * (100 MHz) at start, GLU partials done, hb published, every workgroup's flag
- * seen, hb gathered into LDS, end; then (GLU items | W2 items << 32) of wave 0.
- * *workgroups = grid size. Profiling hook. */
-int yalm_ffn_trace(yalm_decoder d, unsigned long long *host, size_t count, int *workgroups);
-/* Timeline of the engine's most recent launch (decoder created with
- * YALM_ENGINE_TRACE=1): for workgroup w and phase p (5 per layer: QKV,
- * attention, Wo, W1/W3, W2; then logits; the last index 5 L + 1 holds per-CU
- * extras) 8 words at [(w * (5 L + 2) + p) * 8 + k]: s_memrealtime (100 MHz) at
- * phase start / input ready / rows done / published, loader ring-full ticks so
- * far, ring slots landed and consumer item position at phase start.
- * Copies min(count, total) words; *workgroups = grid size. Profiling hook. */
-int yalm_engine_trace(yalm_decoder d, unsigned long long *host, size_t count, int *workgroups);
 
 /* ---------------- tensor parallelism (BASELINE config 5) ----------------
  * Megatron row/column split of one model over tp_size GPUs, one process per

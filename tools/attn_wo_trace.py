@@ -2,7 +2,7 @@
 synthetic model: the last layer's launch of the last token, from the
 per-workgroup s_memrealtime stamps (100 MHz) of yalm_attn_wo_trace.
 
-usage: python tools/attn_wo_trace.py [--model mistral-7b] [--ctx 150] [--form gran|local]
+usage: python tools/attn_wo_trace.py [--model mistral-7b] [--ctx 150] [--dtype fp16|fp8]
 """
 import argparse
 import os
@@ -26,27 +26,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="mistral-7b")
     ap.add_argument("--ctx", type=int, default=150)
-    ap.add_argument("--form", default="gran", choices=["gran", "local"])
+    ap.add_argument("--dtype", default="fp16", choices=["fp16", "fp8"])
     args = ap.parse_args()
-    os.environ["YALM_AWO_LOCAL"] = "1000000" if args.form == "local" else "0"
     runtime.check(runtime.lib.yalm_set_device(0))
-    cfg = M.PRESETS[args.model].with_(weight_dtype=M.F16)
+    cfg = M.PRESETS[args.model].with_(weight_dtype=M.F16 if args.dtype == "fp16" else M.F8E5M2)
     dm = runtime.DeviceModel.synthetic(cfg, seed=1)
     dec = runtime.Decoder(dm)
     assert dec.attn_wo, "decoder does not run the fused attention + Wo launch"
     for pos in range(args.ctx):
         dec.forward((7 * pos + 1) % cfg.vocab_size, pos, runtime.HYDRATE_KV_CACHE)
     dec.forward(5, args.ctx)
-    if args.form == "local":
-        tr = dec.attn_wo_local_trace().astype(np.int64)
-        us = (tr - tr[:, 0].min()) / 100.0
-        print(f"[{args.model} kv_len {args.ctx + 1}] short-context form, grid {len(tr)}; "
-              f"launch span {us[:, 3].max():.2f} us")
-        for k, name in enumerate(["start", "attention in LDS", "Wo slice landed", "end"]):
-            print(f"{name:17s}{q(us[:, k])}")
-        dec.close()
-        dm.close()
-        return
     tr, na = dec.attn_wo_trace()
     tr = tr.astype(np.int64)
     t0 = tr[:, 0].min()

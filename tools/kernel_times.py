@@ -14,8 +14,7 @@ sys.path.insert(0, ROOT)
 from yalm_amd import models as M  # noqa: E402
 from yalm_amd import runtime  # noqa: E402
 
-KINDS = {0: "QKV", 1: "attention", 2: "Wo", 3: "W1|W3+GLU", 4: "W2", 5: "logits", 7: "fused FFN",
-         8: "attn+Wo gran", 9: "attn+Wo local"}
+KINDS = {0: "QKV", 1: "attention", 2: "Wo", 3: "W1|W3+GLU", 4: "W2", 5: "logits", 8: "attn+Wo gran"}
 
 
 def main():
@@ -34,20 +33,13 @@ def main():
     wb = M.DTYPE_BYTES[cfg.weight_dtype]
     nbytes = {0: (cfg.q_dim + 2 * cfg.kv_dim) * cfg.dim * wb, 2: cfg.dim * cfg.q_dim * wb,
               3: 2 * cfg.hidden_dim * cfg.dim * wb, 4: cfg.dim * cfg.hidden_dim * wb,
-              5: cfg.vocab_size * cfg.dim * wb, 7: 3 * cfg.hidden_dim * cfg.dim * wb,
-              8: cfg.dim * cfg.q_dim * wb, 9: cfg.dim * cfg.q_dim * wb}
+              5: cfg.vocab_size * cfg.dim * wb, 8: cfg.dim * cfg.q_dim * wb}
     env = {k: v for k, v in os.environ.items() if k.startswith("YALM_")}
     print(f"[{args.model} {args.dtype} kv_len {args.ctx + 1}] {env}")
     for kid, name in KINDS.items():
-        if kid == 7 and not dec.ffn:
+        if kid == 8 and not dec.attn_wo:
             continue
-        if kid >= 8 and not dec.attn_wo:
-            continue
-        try:
-            us = dec.time_kernel(kid, args.iters) * 1e3
-        except runtime.YalmError as e:  # e.g. kernel 9 while the short-context form is off
-            print(f"  {kid} {name:10s} skipped: {e}")
-            continue
+        us = dec.time_kernel(kid, args.iters) * 1e3
         gbs = nbytes.get(kid, 0) / (us * 1e-6) / 1e9 if kid in nbytes else 0
         print(f"  {kid} {name:10s} {us:8.2f} us  {gbs:7.0f} GB/s  {dec.kernel_name(kid)}")
     dec.close()

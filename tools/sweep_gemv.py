@@ -14,11 +14,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--dtype", default="fp16")
 ap.add_argument("--iters", type=int, default=64)
 ap.add_argument("--kinds", default="0,1,2,3,4")
-ap.add_argument("--legacy", action="store_true", help="sweep the legacy stream kernel (YALM_GEMV_LEGACY=1)")
 ap.add_argument("--top", type=int, default=6)
 args = ap.parse_args()
-if args.legacy:
-    os.environ["YALM_GEMV_LEGACY"] = "1"
 
 cfg = M.MISTRAL_7B.with_(weight_dtype=M.F16 if args.dtype == "fp16" else M.F8E5M2)
 wb = M.DTYPE_BYTES[cfg.weight_dtype]
@@ -39,11 +36,9 @@ for kind in [int(k) for k in args.kinds.split(",")]:
     auto = dec.time_kernel(kid, args.iters)
     print(f"{name}: auto {auto * 1e3:8.2f} us  {nbytes / auto / 1e6:7.0f} GB/s", flush=True)
     results = []
-    for threads in ((256, 512) if args.legacy else (256, 512, 1024)):
-        for unroll in ((4, 8) if args.legacy else (2, 4, 8)):
-            for gpw in (sorted(set([1, 2, 3, 4, 6, 7, 8, 12, 14, 16, 28, 32])) if args.legacy else (1, 2, 3, 4)):
-                if args.legacy and (groups + gpw - 1) // gpw < 256:
-                    continue
+    for threads in (256, 512, 1024):
+        for unroll in (2, 4, 8):
+            for gpw in (1, 2, 3, 4):
                 try:
                     dec.set_gemv_config(kind, threads, unroll, gpw)
                     t = dec.time_kernel(kid, args.iters)
@@ -53,7 +48,7 @@ for kind in [int(k) for k in args.kinds.split(",")]:
                 results.append((t, threads, unroll, gpw))
     results.sort()
     for t, threads, unroll, gpw in results[:args.top]:
-        print(f"   threads={threads} U={unroll} {'gpw' if args.legacy else 'wg/cu'}={gpw:3d}: {t * 1e3:8.2f} us {nbytes / t / 1e6:7.0f} GB/s")
+        print(f"   threads={threads} U={unroll} wg/cu={gpw:3d}: {t * 1e3:8.2f} us {nbytes / t / 1e6:7.0f} GB/s")
     dec.set_gemv_config(kind)
 dec.close()
 dm.close()

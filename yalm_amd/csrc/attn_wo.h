@@ -37,7 +37,7 @@
 #pragma once
 
 #include "attention.h"
-#include "engine.h"
+#include "device_common.h"
 
 #define AWO_RPW 16                   // Wo rows per Wo workgroup (256 of them for Mistral-7B)
 #define AWO_TIMEOUT 200000000ull     // 2 s of s_memrealtime (100 MHz)
@@ -62,6 +62,13 @@ struct AttnWoArgs {
 
 // Eight 16-byte sc1 loads from arbitrary addresses in one statement, one vmcnt(0)
 // (hipcc does not track asm loads: the statement drains its own).
+// Single-copy atomicity assumption: each 16-byte load covers two 8-byte granules,
+// each written by ONE 64-bit atomic store of {value, tag}. Correctness needs the
+// load to see each granule whole (never the new tag with the old value). The HIP
+// memory model does not promise this for a plain asm load racing an atomic store;
+// gfx950 delivers it (MI355X_MICROARCH.md:190, "observed untorn on gfx950 / ROCm
+// 7.2, also for 16-B sc1"), and tests/test_gpu_attn_wo.py::test_attn_wo_stress
+// replays many forwards at high split counts against the separate-launch path.
 __device__ __forceinline__ void awo_ld8_sc1(u32x4_t (&v)[8], const void *const (&a)[8]) {
 	asm volatile("global_load_dwordx4 %0, %8, off sc1\n\t"
 	             "global_load_dwordx4 %1, %9, off sc1\n\t"
@@ -257,7 +264,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 		a0[r] = a1[r] = 0.0f;
 #pragma unroll
 		for (int k = 0; k < XS; ++k)
-			eng_dot16<WT>(a0[r], a1[r], wr[r * XS + k], xs[k]);
+			dot16_mix<WT>(a0[r], a1[r], wr[r * XS + k], xs[k]);
 	}
 	// ---- resident rows . slice; 4-row transposed wave reductions; fixed-order workgroup sum
 #pragma unroll
@@ -266,7 +273,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 #pragma unroll
 		for (int t = 0; t < 4; ++t)
 			acc[t] = a0[r0 + t] + a1[r0 + t];
-		const float tot = eng_sum4_t(acc); // lanes 16 g .. 16 g + 15: row r0 + g
+		const float tot = sum4_t(acc); // lanes 16 g .. 16 g + 15: row r0 + g
 		if ((lane & 15) == 0)
 			rowpart[r0 + (lane >> 4)][wave] = tot;
 	}

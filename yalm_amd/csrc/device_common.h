@@ -161,6 +161,47 @@ struct WF8 {
 	}
 };
 
+// acc += w . x over one 16-byte weight piece, two independent chains (a0: even
+// elements, a1: odd). f16: v_fma_mix_f32 widens the f16 operand exactly and
+// rounds once, so it equals cvt + fma bit for bit at half the instruction count;
+// one asm statement so no compiler padding lands between the dependent ops.
+template <class WT>
+__device__ __forceinline__ void dot16_mix(float &a0, float &a1, const u32x4_t &w, const float (&x)[WT::EPL]) {
+	if constexpr (WT::BYTES == 2) {
+		asm("v_fma_mix_f32 %0, %2, %4, %0 op_sel_hi:[1,0,0]\n\t"
+		    "v_fma_mix_f32 %1, %2, %5, %1 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+		    "v_fma_mix_f32 %0, %3, %6, %0 op_sel_hi:[1,0,0]\n\t"
+		    "v_fma_mix_f32 %1, %3, %7, %1 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+		    : "+v"(a0), "+v"(a1)
+		    : "v"(w[0]), "v"(w[1]), "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]));
+		asm("v_fma_mix_f32 %0, %2, %4, %0 op_sel_hi:[1,0,0]\n\t"
+		    "v_fma_mix_f32 %1, %2, %5, %1 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+		    "v_fma_mix_f32 %0, %3, %6, %0 op_sel_hi:[1,0,0]\n\t"
+		    "v_fma_mix_f32 %1, %3, %7, %1 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+		    : "+v"(a0), "+v"(a1)
+		    : "v"(w[2]), "v"(w[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]));
+	} else {
+		float wf[WT::EPL];
+		WT::unpack(w, wf);
+#pragma unroll
+		for (int e = 0; e < WT::EPL; e += 2) {
+			a0 = fmaf(wf[e], x[e], a0);
+			a1 = fmaf(wf[e + 1], x[e + 1], a1);
+		}
+	}
+}
+
+// Sums of 4 per-lane values over the wave, transposed: lanes 16 t .. 16 t + 15 end
+// with the total of v[t]. Each exchange sends the value the partner keeps and keeps
+// the one it sends back (2 xor-32 + 1 xor-16 lane swaps), then one 16-lane DPP sum.
+__device__ __forceinline__ float sum4_t(const float (&v)[4]) {
+	const bool hi32 = threadIdx.x & 32, odd16 = threadIdx.x & 16;
+	const float s02 = (hi32 ? v[2] : v[0]) + xor32(hi32 ? v[0] : v[2]); // lanes 0-31: row 0, 32-63: row 2
+	const float s13 = (hi32 ? v[3] : v[1]) + xor32(hi32 ? v[1] : v[3]); // row 1 / row 3
+	const float u = (odd16 ? s13 : s02) + xor16(odd16 ? s02 : s13);     // 16-lane group g: row g
+	return row16_sum(u);
+}
+
 // infer.cu:586-596 semantics (SiLU x/(1+e^-x); GELU tanh approximation).
 template <int ACT>
 __device__ __forceinline__ float act_fn(float x) {

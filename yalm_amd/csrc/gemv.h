@@ -187,12 +187,8 @@ struct PGlu {
 	int n;
 	float *out;
 	int n_groups;
-	int w3_rot = 0; // row-block kernel: stream each workgroup's W3 rows rotated by half its groups (rb_perm)
-	int il = 0;     // w1 = one [hidden][2][n] buffer: W1 row g, then W3 row g (decoder copy, YALM_GLU_INTERLEAVE)
 	__device__ __forceinline__ void prologue() const {}
 	__device__ __forceinline__ const char *row(int g, int r) const {
-		if (il)
-			return w1 + (size_t)(2 * g + r) * n * WT::BYTES;
 		return (r == 0 ? w1 : w3) + (size_t)g * n * WT::BYTES;
 	}
 	__device__ __forceinline__ void finish(int g, const float *acc, int lane) const {
@@ -201,20 +197,6 @@ struct PGlu {
 	}
 	__device__ __forceinline__ void finish_all(int g, const float *acc) const { finish(g, acc, 0); }
 };
-
-// Row-block kernel item order: the local group a (group, row-of-group) item is
-// STREAMED for. Identity, except PGlu with w3_rot: a workgroup reads its W3 rows
-// rotated by half its groups, so the chip-wide W3 window sits hidden_dim / 2 rows
-// away from the W1 window instead of at the same offset of the other matrix
-// (the partials still land at the true (group, row), so results are unchanged).
-template <class P>
-__device__ __forceinline__ int rb_perm(const P &, int gl, int, int) {
-	return gl;
-}
-template <class WT, int ACT>
-__device__ __forceinline__ int rb_perm(const PGlu<WT, ACT> &p, int gl, int r, int ngl) {
-	return r == 1 && p.w3_rot ? (gl + (ngl >> 1)) % ngl : gl;
-}
 
 // Rotate the attention-sink keys by one position (infer.cpp:303-317,
 // infer.cu:679-697), executed by workgroup 0 of the QKV launch. Rows < kv_sink
@@ -439,103 +421,6 @@ __global__ __launch_bounds__(GEMV_THREADS) void gemv_kernel(P p, const float *__
 	}
 }
 
-// Streaming GEMV (the production path; requires n % (64 * EPL) == 0).
-//
-// Each wave owns `gpw` consecutive row groups and walks them as ONE flattened
-// stream of 16-byte-per-lane chunks with U chunk-slots of R rows kept in
-// flight: slot u is refilled with chunk k+U right after chunk k is consumed,
-// so the HBM queue never drains at row boundaries. The first U slots are
-// issued before the x staging / rmsnorm prologue so weight latency overlaps
-// it. With the host picking (THREADS, gpw) such that every workgroup of the
-// launch is resident at once (one "wave" of workgroups, choose_gemv_cfg), the
-// per-CU work is balanced to within one row group and there is no tail.
-template <class WT, class P, int U, bool NORM, int THREADS>
-__global__ __launch_bounds__(THREADS) void gemv_stream_kernel(P p, const float *__restrict__ x,
-                                                              const float *__restrict__ normw, float eps, int gpw) {
-	extern __shared__ __attribute__((aligned(16))) float xs[];
-	constexpr int R = P::R;
-	constexpr int EPL = WT::EPL;
-	constexpr int CH = YALM_WAVE * EPL;
-	constexpr size_t CHB = (size_t)CH * WT::BYTES;
-	const int n = p.n;
-	const int nch = n / CH;
-	const int lane = threadIdx.x & 63;
-	const int wave = threadIdx.x >> 6;
-	const int g0 = (blockIdx.x * (THREADS / YALM_WAVE) + wave) * gpw;
-	const int gend = min(g0 + gpw, p.n_groups);
-	const int total = gend > g0 ? (gend - g0) * nch : 0;
-	const size_t lane_off = (size_t)lane * EPL * WT::BYTES;
-
-	int ig = g0, ic = 0; // issue cursor (group, chunk)
-	const char *rp[R];
-#pragma unroll
-	for (int r = 0; r < R; ++r)
-		rp[r] = nullptr;
-	if (total > 0) {
-#pragma unroll
-		for (int r = 0; r < R; ++r)
-			rp[r] = p.row(ig, r) + lane_off;
-	}
-	u32x4_t buf[U][R];
-#pragma unroll
-	for (int u = 0; u < U; ++u) {
-		if (u < total) {
-#pragma unroll
-			for (int r = 0; r < R; ++r)
-				buf[u][r] = load_nt16(rp[r] + ic * CHB);
-			if (++ic == nch) {
-				ic = 0;
-				if (++ig < gend) {
-#pragma unroll
-					for (int r = 0; r < R; ++r)
-						rp[r] = p.row(ig, r) + lane_off;
-				}
-			}
-		}
-	}
-
-	p.prologue();
-	stage_x<NORM>(xs, x, normw, n, eps);
-
-	float acc[R];
-#pragma unroll
-	for (int r = 0; r < R; ++r)
-		acc[r] = 0.0f;
-	int cg = g0, cc = 0; // consume cursor
-	for (int k = 0; k < total; k += U) {
-#pragma unroll
-		for (int u = 0; u < U; ++u) {
-			if (k + u < total) {
-				fma_chunk<WT, R>(acc, buf[u], xs + cc * CH + lane * EPL);
-				if (k + u + U < total) {
-#pragma unroll
-					for (int r = 0; r < R; ++r)
-						buf[u][r] = load_nt16(rp[r] + ic * CHB);
-					if (++ic == nch) {
-						ic = 0;
-						if (++ig < gend) {
-#pragma unroll
-							for (int r = 0; r < R; ++r)
-								rp[r] = p.row(ig, r) + lane_off;
-						}
-					}
-				}
-				if (++cc == nch) {
-#pragma unroll
-					for (int r = 0; r < R; ++r)
-						acc[r] = wave_sum(acc[r]);
-					p.finish(cg, acc, lane);
-#pragma unroll
-					for (int r = 0; r < R; ++r)
-						acc[r] = 0.0f;
-					cc = 0;
-					++cg;
-				}
-			}
-		}
-	}
-}
-
 // Row-block GEMV — the production path (n % (64 * EPL) == 0).
 //
 // One workgroup per CU (gridDim.x = NB ~ CU count): row group g belongs to
@@ -586,12 +471,9 @@ __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__re
 	};
 	auto iaddr = [&](int vr, int c) {
 		const int gl = vr / R, r = vr - gl * R;
-		return p.row(b + rb_perm(p, gl, r, ngl) * NB, r) + (size_t)c * CHB + lane_off;
+		return p.row(b + gl * NB, r) + (size_t)c * CHB + lane_off;
 	};
-	auto pslot = [&](int vr) { // LDS partial slot of item row vr: its true (group, row)
-		const int gl = vr / R, r = vr - gl * R;
-		return (rb_perm(p, gl, r, ngl) * R + r) * W + wave;
-	};
+	auto pslot = [&](int vr) { return vr * W + wave; }; // LDS partial slot of item row vr
 
 	int ivr = wave / nch, ic = wave - (wave / nch) * nch; // issue cursor
 	const int vr0 = ivr, c0 = ic;

@@ -24,6 +24,12 @@ __global__ void set_step_full_kernel(StepState *st, int pos, int kv_sink, int kv
 	st->epoch = st->epoch + 1u;
 }
 
+// Timing hook (yalm_time_kernel): a new launch generation, as step_begin_kernel
+// starts one, so an in-launch hand-off never sees the previous launch's tags.
+__global__ void epoch_bump_kernel(StepState *st) {
+	st->epoch = st->epoch + 1u;
+}
+
 // First node of every forward graph: sliding-window indices (infer.cu:1081-
 // 1083; KV_SINKS = 2, model.h:12) and x = embedding[token] (infer.cu:622-640).
 template <class WT>

@@ -20,9 +20,7 @@
 #include "attn_wo.h"
 #include "decoder.h"
 #include "device_common.h"
-#include "ffn.h"
 #include "gemv.h"
-#include "gemv_dyn.h"
 #include "misc_kernels.h"
 
 // ------------------------------------------------------------------ errors
@@ -128,73 +126,6 @@ int device_cu_count() {
 	return n;
 }
 
-// Default geometry: many small workgroups, one row group per wave, U = 4
-// chunks in flight per row — the hardware dispatcher then balances the CUs
-// dynamically. Measured on MI355X (tools/sweep_gemv.py, profiles/) this beats
-// the "one resident wave of workgroups" geometry of balanced_gemv_cfg by
-// 3-10% on every Mistral-7B GEMV, matching the pure-read streaming envelope
-// of tools/stream_bench.hip (4-16 KB per wave is the sweet spot).
-static GemvCfg default_gemv_cfg(int kind) {
-	if (kind == GK_WO)
-		return GemvCfg{256, 8, 1};
-	if (kind == GK_CLS)
-		return GemvCfg{256, 4, 6};
-	return GemvCfg{512, 4, 1};
-}
-
-// Alternative geometry (tuning hook, threads/gpw = 0 in yalm_set_gemv_config
-// with YALM_GEMV_BALANCED=1): all workgroups resident at once, the busiest CU
-// holding as few row groups as possible, 8..16 waves per CU.
-static GemvCfg balanced_gemv_cfg(int n_groups, size_t lds_bytes, GemvCfg want) {
-	const int ncu = device_cu_count();
-	GemvCfg best;
-	long best_cost = -1;
-	int best_waves = 0;
-	for (int threads : {512, 256}) {
-		if (want.threads && threads != want.threads)
-			continue;
-		const int wpw = threads / YALM_WAVE;
-		const int lds_fit = (int)std::max<size_t>(1, 163840 / std::max<size_t>(lds_bytes, 1));
-		for (int gpw = 1; gpw <= 256; ++gpw) {
-			if (want.gpw && gpw != want.gpw)
-				continue;
-			const long nw = (n_groups + gpw - 1) / gpw;
-			const long nwg = (nw + wpw - 1) / wpw;
-			const long per_cu_wg = (nwg + ncu - 1) / ncu;
-			const long waves_cu = per_cu_wg * wpw;
-			if (per_cu_wg > lds_fit || waves_cu > 16)
-				continue;
-			const long cost = per_cu_wg * wpw * gpw;
-			const bool enough = waves_cu >= 8;
-			const bool best_enough = best_waves >= 8;
-			if (best_cost < 0 || (enough && !best_enough) ||
-			    (enough == best_enough && (cost < best_cost || (cost == best_cost && waves_cu > best_waves)))) {
-				best_cost = cost;
-				best = GemvCfg{threads, 0, gpw};
-				best_waves = (int)waves_cu;
-			}
-		}
-	}
-	if (best_cost < 0)
-		best = GemvCfg{256, 0, std::max(1, (n_groups + ncu * 16 - 1) / (ncu * 16))};
-	best.U = want.U ? want.U : 8;
-	return best;
-}
-
-template <class WT, class P, bool NORM, int THREADS, int U>
-static int launch_stream(const P &p, const float *x, const float *normw, float eps, int gpw, size_t lds,
-                         hipStream_t st) {
-	auto kern = gemv_stream_kernel<WT, P, U, NORM, THREADS>;
-	if (lds > 65536)
-		HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-	const int waves = THREADS / YALM_WAVE;
-	const long nw = (p.n_groups + gpw - 1) / gpw;
-	const int blocks = (int)((nw + waves - 1) / waves);
-	hipLaunchKernelGGL(kern, dim3(blocks), dim3(THREADS), lds, st, p, x, normw, eps, gpw);
-	HIPCHK(hipGetLastError());
-	return YALM_OK;
-}
-
 // Row-block geometry (gemv_rb_kernel): `gpw` = workgroups per CU (default 1),
 // threads 512 (8 waves), U = 8 loads in flight per wave.
 template <class WT, class P, bool NORM, int THREADS, int U>
@@ -278,34 +209,13 @@ static int launch_gemv(const P &p, const float *x, const float *normw, float eps
 		HIPCHK(hipGetLastError());
 		return YALM_OK;
 	}
-	static const bool legacy = getenv("YALM_GEMV_LEGACY") && atoi(getenv("YALM_GEMV_LEGACY")) != 0;
-	if (!legacy)
-		return launch_rb<WT, P, NORM>(p, x, normw, eps, kind, want, st);
-	static const bool balanced = getenv("YALM_GEMV_BALANCED") && atoi(getenv("YALM_GEMV_BALANCED")) != 0;
-	const GemvCfg def = balanced ? balanced_gemv_cfg(p.n_groups, lds, want) : default_gemv_cfg(kind);
-	GemvCfg c;
-	c.threads = want.threads ? want.threads : def.threads;
-	c.U = want.U ? want.U : def.U;
-	c.gpw = want.gpw ? want.gpw : def.gpw;
-	if (c.threads == 512)
-		return c.U == 4 ? launch_stream<WT, P, NORM, 512, 4>(p, x, normw, eps, c.gpw, lds, st)
-		                : launch_stream<WT, P, NORM, 512, 8>(p, x, normw, eps, c.gpw, lds, st);
-	return c.U == 4 ? launch_stream<WT, P, NORM, 256, 4>(p, x, normw, eps, c.gpw, lds, st)
-	                : launch_stream<WT, P, NORM, 256, 8>(p, x, normw, eps, c.gpw, lds, st);
+	return launch_rb<WT, P, NORM>(p, x, normw, eps, kind, want, st);
 }
 
-// The decoder's weight-streaming GEMVs: the work-stealing row-block kernel
-// (gemv_dyn.h) when enabled and the shape fits, else gemv_rb_kernel (or the
-// geometry set through yalm_set_gemv_config).
+// The decoder's weight-streaming GEMVs: gemv_rb_kernel with the geometry set
+// through yalm_set_gemv_config (or the per-kind default).
 template <class WT, class P, bool NORM>
 static int launch_gemv_d(yalm_decoder_s *d, const P &p, const float *x, const float *normw, float eps, int kind) {
-	if constexpr (WT::BYTES <= 2) {
-		if (d->dyn && !d->gemv[kind].threads) {
-			const int r = launch_dyn<WT, P, NORM>(p, x, normw, eps, d->dyn_ctr, d->dyn_frac, d->stream);
-			if (r != DYN_FALLBACK)
-				return r;
-		}
-	}
 	return launch_gemv<WT, P, NORM>(p, x, normw, eps, kind, d->gemv[kind], d->stream);
 }
 
@@ -432,27 +342,41 @@ static int attn_wo_init(yalm_decoder_s *d) {
 	// stream (tools/sweep_awo.sh, profiles/r2_sweep_awo_delay.txt: 10.6 -> 10.1 us at kv_len 17,
 	// 10.6 -> 10.4 at kv_len 151; 0.4-0.6 us delays lose it again at long contexts)
 	d->awo_delay = denv ? std::max(0, atoi(denv)) : 20;
+	// speculative gather (opt-in): the round-2 A/B that made it the default timed
+	// back-to-back launches whose granules already held the current epoch, i.e. with no
+	// attention -> Wo dependency; yalm_time_kernel now advances the epoch per launch
 	const char *spenv = getenv("YALM_AWO_SPEC");
-	d->awo_spec = spenv ? atoi(spenv) != 0 : 1; // profiles/r2c_ab_awo_spec.txt: 10.17 -> 9.76 us (kv 17)
+	d->awo_spec = spenv ? atoi(spenv) != 0 : 0;
 	const char *tenv = getenv("YALM_ATTN_WO_TRACE");
 	if (tenv && atoi(tenv) != 0)
 		TRY(dalloc(d, (void **)&d->awo_trace, sizeof(unsigned long long) * 4 * d->awo_nb));
-	// short-context form (attn_wo_local_kernel): every Wo workgroup recomputes the attention
-	// from L2 while its slice streams in; the host picks it per token while kv_len <= this
-	// (YALM_AWO_LOCAL, opt-in: 0 = never; any value is correct, the kernel loops over 32-key
-	// blocks). Measured slower on MI355X (Mistral-7B fp16, kv_len 17: 16-20 us per launch vs
-	// 10.7 for the granule form): 256 CUs each re-reading every head's K/V
-	// from L2 (~4 MB per XCD per 32-key block) and the replicated softmax cost more than
-	// the hand-off they remove.
-	const char *lenv = getenv("YALM_AWO_LOCAL");
-	d->awo_local_max = lenv ? std::max(0, atoi(lenv)) : 0;
-	const char *kfenv = getenv("YALM_AWL_KV_FIRST");
-	d->awl_kv_first = kfenv ? atoi(kfenv) != 0 : 1;
-	if (d->awo_local_max > 0 && attn_wo_local_occupancy(c.weight_dtype, G, rb / 4096) < 1)
-		d->awo_local_max = 0;
-	if (d->awo_local_max > 0 && tenv && atoi(tenv) != 0)
-		TRY(dalloc(d, (void **)&d->awl_trace, sizeof(unsigned long long) * 4 * ((c.dim + AWO_RPW - 1) / AWO_RPW)));
 	d->attn_wo = true;
+	return YALM_OK;
+}
+
+// After a sync: report (once) a bounded spin that gave up -- the fused attention + Wo
+// launch waiting for its heads, or an IPC exchange waiting for a peer.
+int awo_check(yalm_decoder_s *d) {
+	if (d->awo_err) {
+		unsigned e = 0;
+		HIPCHK(hipMemcpy(&e, d->awo_err, sizeof(e), hipMemcpyDeviceToHost));
+		if (e) { // cleared so that later calls report only their own failures
+			HIPCHK(hipMemset(d->awo_err, 0, sizeof(e)));
+			set_err("fused attention + Wo launch gave up waiting for the attention heads (error bits " +
+			        std::to_string(e) + "); YALM_ATTN_WO=0 selects separate launches");
+			return YALM_ERR_HIP;
+		}
+	}
+	if (d->ipc) {
+		unsigned *flag = (unsigned *)(d->ipc_own + 2 * (size_t)d->ipc_S) + 63;
+		unsigned e = 0;
+		HIPCHK(hipMemcpy(&e, flag, sizeof(e), hipMemcpyDeviceToHost));
+		if (e) {
+			HIPCHK(hipMemset(flag, 0, sizeof(e)));
+			set_err("tensor-parallel IPC exchange gave up waiting for a peer rank (results invalid)");
+			return YALM_ERR_HIP;
+		}
+	}
 	return YALM_OK;
 }
 
@@ -473,8 +397,6 @@ static void launch_attn_wo_g(yalm_decoder_s *d, const yalm_block_weights &w, con
 }
 template <class WT>
 static int launch_attn_wo(yalm_decoder_s *d, const yalm_block_weights &w, int layer) {
-	if (d->awo_local_now)
-		return launch_attn_wo_local(d, w);
 	const yalm_config &c = d->c;
 	AttnWoArgs p;
 	p.n_heads = c.n_heads;
@@ -502,97 +424,6 @@ static int launch_attn_wo(yalm_decoder_s *d, const yalm_block_weights &w, int la
 			launch_attn_wo_g<WT, 2>(d, w, p, G);
 	}
 	HIPCHK(hipGetLastError());
-	return YALM_OK;
-}
-
-// ---- rmsnorm + GLU + W2 + residual in one launch (ffn.h)
-#define FFN_U 4
-template <class WT, int ACT>
-static const void *ffn_fn(int P) {
-	switch (P) {
-	case 0:
-		return (const void *)ffn_kernel<WT, ACT, FFN_U, 0>;
-	case 4:
-		return (const void *)ffn_kernel<WT, ACT, FFN_U, 4>;
-	case 12:
-		return (const void *)ffn_kernel<WT, ACT, FFN_U, 12>;
-	default:
-		return (const void *)ffn_kernel<WT, ACT, FFN_U, 8>;
-	}
-}
-static const void *ffn_pick(int dtype, int act, int P) {
-	if (dtype == YALM_F16)
-		return act == YALM_SILU ? ffn_fn<WF16, 1>(P) : ffn_fn<WF16, 0>(P);
-	return act == YALM_SILU ? ffn_fn<WF8, 1>(P) : ffn_fn<WF8, 0>(P);
-}
-
-// Single-GPU decoders with fp16 / fp8 weights and dim, hidden_dim multiples of
-// one 1-KB chunk per wave instruction (512 fp16 / 1024 fp8 elements).
-static int ffn_init(yalm_decoder_s *d) {
-	const yalm_config &c = d->c;
-	// opt-in (YALM_FFN=1): measured slower than the separate launches on MI355X
-	// (Mistral-7B fp16: 59.5-61 us per launch against 38.7 + 20.8 us):
-	// the in-launch seam (slowest workgroup + hb publish + flag propagation + gather,
-	// ~6 us) costs more than the kernel boundary it replaces
-	const char *env = getenv("YALM_FFN");
-	if (!env || atoi(env) == 0)
-		return YALM_OK;
-	if (d->comm || d->ipc || d->tp_size > 1 || d->engine)
-		return YALM_OK;
-	if (c.weight_dtype != YALM_F16 && c.weight_dtype != YALM_F8E5M2)
-		return YALM_OK;
-	const int CH = c.weight_dtype == YALM_F16 ? 512 : 1024;
-	if (c.dim % CH != 0 || c.hidden_dim % CH != 0)
-		return YALM_OK;
-	const char *penv = getenv("YALM_FFN_P");
-	const int P = penv ? atoi(penv) : 8;
-	if (P != 0 && P != 4 && P != 8 && P != 12) {
-		set_err("YALM_FFN_P must be 0, 4, 8 or 12");
-		return YALM_ERR_ARG;
-	}
-	const int nb = device_cu_count();
-	const size_t lds = ffn_lds_floats(c.dim, c.hidden_dim, nb) * sizeof(float);
-	if (lds > 160 * 1024)
-		return YALM_OK;
-	const void *fn = ffn_pick(c.weight_dtype, c.act, P);
-	if (lds > 65536)
-		HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-	// the seam waits on every workgroup: the whole grid (one per CU) must be resident
-	int occ = 0;
-	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, FFN_THREADS, lds) != hipSuccess || occ < 1)
-		return YALM_OK;
-	d->ffn_nb = nb;
-	d->ffn_P = P;
-	d->ffn_lds = lds;
-	TRY(dalloc(d, (void **)&d->ffn_flags, sizeof(unsigned) * ((size_t)c.n_layers * nb + 64)));
-	d->ffn_err = d->ffn_flags + (size_t)c.n_layers * nb;
-	const char *tenv = getenv("YALM_FFN_TRACE");
-	if (tenv && atoi(tenv) != 0)
-		TRY(dalloc(d, (void **)&d->ffn_trace, sizeof(unsigned long long) * FFN_TRACE_WORDS * nb));
-	d->ffn = true;
-	return YALM_OK;
-}
-
-template <class WT>
-static int launch_ffn(yalm_decoder_s *d, const yalm_block_weights &w, int layer) {
-	const yalm_config &c = d->c;
-	FfnArgs p;
-	p.w1 = (const char *)w.w1;
-	p.w3 = (const char *)w.w3;
-	p.w2 = (const char *)w.w2;
-	p.normw = w.rms_ffn;
-	p.eps = c.norm_eps;
-	p.x = d->x;
-	p.hb = d->hb;
-	p.flags = d->ffn_flags + (size_t)layer * d->ffn_nb;
-	p.err = d->ffn_err;
-	p.step = d->step;
-	p.dim = c.dim;
-	p.hidden = c.hidden_dim;
-	p.trace = d->ffn_trace;
-	const void *fn = ffn_pick(c.weight_dtype, c.act, d->ffn_P);
-	void *args[] = {&p};
-	HIPCHK(hipLaunchKernel(fn, dim3(d->ffn_nb), dim3(FFN_THREADS), args, d->ffn_lds, d->stream));
 	return YALM_OK;
 }
 
@@ -689,11 +520,6 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 		if (!(ab & 4))
 			TRY(enqueue_residual_gemv<WT>(d, w.wo, q_dim, d->xb2, GK_WO));
 	}
-	if (d->ffn && WT::BYTES <= 2) {
-		if (!(ab & 24))
-			TRY(launch_ffn<WT>(d, w, l));
-		return YALM_OK;
-	}
 	if (ab & 8) {
 	} else if (c.act == YALM_SILU) {
 		PGlu<WT, 1> p;
@@ -702,11 +528,6 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 		p.n = c.dim;
 		p.out = d->hb;
 		p.n_groups = c.hidden_dim;
-		p.w3_rot = d->glu_w3_rot;
-		if (!d->glu_il.empty()) {
-			p.w1 = (const char *)d->glu_il[l];
-			p.il = 1;
-		}
 		TRY((launch_gemv_d<WT, PGlu<WT, 1>, true>(d, p, d->x, w.rms_ffn, c.norm_eps, GK_GLU)));
 	} else {
 		PGlu<WT, 0> p;
@@ -715,11 +536,6 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 		p.n = c.dim;
 		p.out = d->hb;
 		p.n_groups = c.hidden_dim;
-		p.w3_rot = d->glu_w3_rot;
-		if (!d->glu_il.empty()) {
-			p.w1 = (const char *)d->glu_il[l];
-			p.il = 1;
-		}
 		TRY((launch_gemv_d<WT, PGlu<WT, 0>, true>(d, p, d->x, w.rms_ffn, c.norm_eps, GK_GLU)));
 	}
 	if (!(ab & 16))
@@ -772,13 +588,6 @@ static int enqueue_begin_t(yalm_decoder_s *d) {
 	                       : FN<WF8>(__VA_ARGS__))
 
 static int enqueue_forward(yalm_decoder_s *d, int which) {
-	if (d->engine) {
-		TRY(engine_enqueue(d, which));
-		if (which == GRAPH_LOGITS)
-			HIPCHK(hipMemcpyAsync(d->logits_pinned, d->logits, sizeof(float) * d->vocab_full, hipMemcpyDeviceToHost,
-			                      d->stream));
-		return YALM_OK;
-	}
 	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_begin_t, d));
 	for (int l = 0; l < d->c.n_layers; ++l)
 		TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_layer_t, d, l));
@@ -830,18 +639,8 @@ static int enqueue_forward(yalm_decoder_s *d, int which) {
 	return YALM_OK;
 }
 
-// Which attention + Wo form the forward at position pos runs (the host tracks the
-// position; both forms are correct at any kv_len, the choice is speed only).
-static bool use_local_at(const yalm_decoder_s *d, long long pos) {
-	if (!d->attn_wo || d->awo_local_max <= 0 || pos < 0)
-		return false;
-	const long long kv_len = pos >= d->c.max_seq_len ? d->c.max_seq_len : pos + 1;
-	return kv_len <= d->awo_local_max;
-}
-
 static int ensure_graph(yalm_decoder_s *d, int which) {
-	const int v = d->awo_local_now ? 1 : 0;
-	if (d->exec[v][which] || d->eager)
+	if (d->exec[which] || d->eager)
 		return YALM_OK;
 	HIPCHK(hipStreamBeginCapture(d->stream, hipStreamCaptureModeRelaxed));
 	int r = enqueue_forward(d, which);
@@ -850,22 +649,20 @@ static int ensure_graph(yalm_decoder_s *d, int which) {
 	if (r != YALM_OK)
 		return r;
 	HIPCHK(e);
-	d->graph[v][which] = g;
-	HIPCHK(hipGraphInstantiate(&d->exec[v][which], g, nullptr, nullptr, 0));
+	d->graph[which] = g;
+	HIPCHK(hipGraphInstantiate(&d->exec[which], g, nullptr, nullptr, 0));
 	return YALM_OK;
 }
 
-// Both attention + Wo forms of graph `which` (captured before any replay is queued).
-static int ensure_graphs(yalm_decoder_s *d, int which) {
-	const bool now = d->awo_local_now;
-	d->awo_local_now = false;
-	int r = ensure_graph(d, which);
-	if (r == YALM_OK && d->attn_wo && d->awo_local_max > 0) {
-		d->awo_local_now = true;
-		r = ensure_graph(d, which);
+static void drop_graphs(yalm_decoder_s *d) {
+	for (int i = 0; i < N_GRAPHS; ++i) {
+		if (d->exec[i])
+			(void)hipGraphExecDestroy(d->exec[i]);
+		if (d->graph[i])
+			(void)hipGraphDestroy(d->graph[i]);
+		d->exec[i] = nullptr;
+		d->graph[i] = nullptr;
 	}
-	d->awo_local_now = now;
-	return r;
 }
 
 static int validate_config(const yalm_config *c) {
@@ -886,14 +683,7 @@ static int validate_config(const yalm_config *c) {
 }
 
 static void destroy_decoder(yalm_decoder_s *d) {
-	for (int v = 0; v < 2; ++v) {
-		for (int i = 0; i < N_GRAPHS; ++i) {
-			if (d->exec[v][i])
-				(void)hipGraphExecDestroy(d->exec[v][i]);
-			if (d->graph[v][i])
-				(void)hipGraphDestroy(d->graph[v][i]);
-		}
-	}
+	drop_graphs(d);
 	if (d->comm)
 		(void)ncclCommDestroy((ncclComm_t)d->comm);
 	for (void *p : d->ipc_opened)
@@ -921,7 +711,7 @@ int dalloc(yalm_decoder_s *d, void **p, size_t bytes) {
 static int replay(yalm_decoder_s *d, int which) {
 	if (d->eager)
 		return enqueue_forward(d, which);
-	HIPCHK(hipGraphLaunch(d->exec[d->awo_local_now ? 1 : 0][which], d->stream));
+	HIPCHK(hipGraphLaunch(d->exec[which], d->stream));
 	if (d->graph_sync)
 		HIPCHK(hipStreamSynchronize(d->stream));
 	return YALM_OK;
@@ -964,7 +754,6 @@ static int create_decoder(const yalm_config *config, const yalm_model_weights *w
 	d->eager = getenv("YALM_EAGER") && atoi(getenv("YALM_EAGER")) != 0;
 	d->graph_sync = getenv("YALM_GRAPH_SYNC") && atoi(getenv("YALM_GRAPH_SYNC")) != 0;
 	d->ablate = getenv("YALM_ABLATE") ? atoi(getenv("YALM_ABLATE")) : 0;
-	d->glu_w3_rot = getenv("YALM_GLU_W3_ROT") ? atoi(getenv("YALM_GLU_W3_ROT")) != 0 : 0;
 	// geometry overrides for A/B runs without a rebuild (same meaning as yalm_set_gemv_config):
 	// YALM_GEMV_CFG="kind:threads:unroll:gpw[,kind:threads:unroll:gpw...]", kind 0..4
 	if (const char *g = getenv("YALM_GEMV_CFG")) {
@@ -1013,39 +802,8 @@ static int create_decoder(const yalm_config *config, const yalm_model_weights *w
 		set_err("hipHostMalloc failed");
 		return fail(YALM_ERR_HIP);
 	}
-	if ((r = engine_init(d)) || (r = attn_wo_init(d)) || (r = ffn_init(d)))
+	if ((r = attn_wo_init(d)))
 		return fail(r);
-	// opt-in: W1 and W3 interleaved row by row in one decoder-owned buffer per layer, so the
-	// W1|W3 GEMV streams ONE contiguous window (costs a copy of both matrices)
-	if (getenv("YALM_GLU_INTERLEAVE") && atoi(getenv("YALM_GLU_INTERLEAVE")) != 0 && !d->engine && !d->ffn &&
-	    c.weight_dtype != YALM_F32) {
-		const size_t rb = (size_t)c.dim * (c.weight_dtype == YALM_F16 ? 2 : 1);
-		for (int l = 0; l < c.n_layers; ++l) {
-			void *buf = nullptr;
-			if ((r = dalloc(d, &buf, 2 * rb * c.hidden_dim)))
-				return fail(r);
-			if (hipMemcpy2D(buf, 2 * rb, d->b[l].w1, rb, rb, c.hidden_dim, hipMemcpyDeviceToDevice) != hipSuccess ||
-			    hipMemcpy2D((char *)buf + rb, 2 * rb, d->b[l].w3, rb, rb, c.hidden_dim, hipMemcpyDeviceToDevice) !=
-			        hipSuccess) {
-				set_err("GLU interleave copy failed");
-				return fail(YALM_ERR_HIP);
-			}
-			d->glu_il.push_back(buf);
-		}
-	}
-	{ // work-stealing GEMV tail (gemv_dyn.h): single-GPU launch path, fp16 / fp8 weights.
-	  // Opt-in (YALM_DYN=1): measured slower on MI355X (Mistral-7B fp16: QKV 15.1 vs 12.0 us,
-	  // W1|W3 44.4 vs 39.6, W2 23.7 vs 20.8; static prefix alone 1-3 us slower)
-		const char *e = getenv("YALM_DYN");
-		const char *fr = getenv("YALM_DYN_FRAC");
-		d->dyn_frac = fr ? std::max(0, std::min(50, atoi(fr))) : 10;
-		if (e && atoi(e) != 0 && !d->engine && !d->comm && !d->ipc && tp_size == 1 &&
-		    (c.weight_dtype == YALM_F16 || c.weight_dtype == YALM_F8E5M2)) {
-			if ((r = dalloc(d, (void **)&d->dyn_ctr, sizeof(unsigned) * DYN_SHARDS * DYN_STRIDE)))
-				return fail(r);
-			d->dyn = true;
-		}
-	}
 	if (hipDeviceSynchronize() != hipSuccess) {
 		set_err("hipDeviceSynchronize failed after decoder allocation");
 		return fail(YALM_ERR_HIP);
@@ -1155,7 +913,6 @@ extern "C" int yalm_decoder_create_tp_ipc(const yalm_config *config, const yalm_
 	}
 	yalm_decoder_s *d = *out;
 	d->ipc = true;
-	d->engine = false; // the engine is single-GPU only
 	d->ipc_S = ipc_slot_floats(*config, tp_size);
 	d->ipc_own = (float *)own_buf;
 	d->ipc_opened = opened;
@@ -1191,7 +948,6 @@ extern "C" int yalm_forward(yalm_decoder d, int token, int pos, int mode, float 
 	ARGCHK(token >= 0 && token < d->vocab_full, "token out of range");
 	ARGCHK(pos >= 0, "negative pos");
 	const int which = mode == YALM_HYDRATE_KV_CACHE ? GRAPH_HYDRATE : GRAPH_LOGITS;
-	d->awo_local_now = use_local_at(d, pos);
 	TRY(ensure_graph(d, which));
 	set_step_kernel<<<1, 1, 0, d->stream>>>(d->step, token, pos, 0);
 	HIPCHK(hipGetLastError());
@@ -1199,7 +955,7 @@ extern "C" int yalm_forward(yalm_decoder d, int token, int pos, int mode, float 
 	d->host_pos = pos; // OUTPUT / HYDRATE forwards do not advance the device position
 	if (which == GRAPH_LOGITS) {
 		HIPCHK(hipStreamSynchronize(d->stream));
-		TRY(engine_check(d));
+		TRY(awo_check(d));
 		if (logits_host)
 			memcpy(logits_host, d->logits_pinned, sizeof(float) * d->vocab_full);
 	}
@@ -1208,9 +964,8 @@ extern "C" int yalm_forward(yalm_decoder d, int token, int pos, int mode, float 
 
 extern "C" int yalm_enqueue_greedy(yalm_decoder d, int n_steps) {
 	ARGCHK(d, "null decoder");
-	TRY(ensure_graphs(d, GRAPH_GREEDY));
+	TRY(ensure_graph(d, GRAPH_GREEDY));
 	for (int i = 0; i < n_steps; ++i) { // each replay advances the device position by one
-		d->awo_local_now = use_local_at(d, d->host_pos);
 		TRY(replay(d, GRAPH_GREEDY));
 		if (d->host_pos >= 0)
 			++d->host_pos;
@@ -1221,7 +976,7 @@ extern "C" int yalm_enqueue_greedy(yalm_decoder d, int n_steps) {
 extern "C" int yalm_generate_greedy(yalm_decoder d, int token, int pos, int n_steps, int *out_tokens) {
 	ARGCHK(d && out_tokens, "null argument");
 	ARGCHK(token >= 0 && token < d->vocab_full && pos >= 0 && n_steps >= 0, "bad token/pos/n_steps");
-	TRY(ensure_graphs(d, GRAPH_GREEDY));
+	TRY(ensure_graph(d, GRAPH_GREEDY));
 	int done = 0;
 	bool first = true;
 	while (done < n_steps) {
@@ -1232,14 +987,12 @@ extern "C" int yalm_generate_greedy(yalm_decoder d, int token, int pos, int n_st
 			set_step_kernel<<<1, 1, 0, d->stream>>>(d->step, out_tokens[done - 1], pos + done, 1);
 		HIPCHK(hipGetLastError());
 		first = false;
-		for (int i = 0; i < batch; ++i) {
-			d->awo_local_now = use_local_at(d, (long long)pos + done + i);
+		for (int i = 0; i < batch; ++i)
 			TRY(replay(d, GRAPH_GREEDY));
-		}
 		d->host_pos = (long long)pos + done + batch;
 		HIPCHK(hipMemcpyAsync(out_tokens + done, d->tokens, sizeof(int) * batch, hipMemcpyDeviceToHost, d->stream));
 		HIPCHK(hipStreamSynchronize(d->stream));
-		TRY(engine_check(d));
+		TRY(awo_check(d));
 		done += batch;
 	}
 	return YALM_OK;
@@ -1249,7 +1002,7 @@ extern "C" int yalm_device_step(yalm_decoder d, int *token, int *pos) {
 	ARGCHK(d, "null decoder");
 	StepState s;
 	HIPCHK(hipStreamSynchronize(d->stream));
-	TRY(engine_check(d));
+	TRY(awo_check(d));
 	HIPCHK(hipMemcpy(&s, d->step, sizeof(s), hipMemcpyDeviceToHost));
 	if (token)
 		*token = s.token;
@@ -1264,7 +1017,6 @@ extern "C" int yalm_block(yalm_decoder d, int layer, int pos, int kv_sink, int k
 	       "bad kv indices");
 	set_step_full_kernel<<<1, 1, 0, d->stream>>>(d->step, pos, kv_sink, kv_pos, kv_len);
 	HIPCHK(hipGetLastError());
-	d->awo_local_now = d->attn_wo && kv_len <= d->awo_local_max;
 	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_layer_t, d, layer));
 	HIPCHK(hipStreamSynchronize(d->stream));
 	return YALM_OK;
@@ -1335,11 +1087,6 @@ static int enqueue_one_t(yalm_decoder_s *d, int kernel_id, int l) {
 		p.n = c.dim;
 		p.out = d->hb;
 		p.n_groups = c.hidden_dim;
-		p.w3_rot = d->glu_w3_rot;
-		if (!d->glu_il.empty()) {
-			p.w1 = (const char *)d->glu_il[l];
-			p.il = 1;
-		}
 		return launch_gemv_d<WT, PGlu<WT, 1>, true>(d, p, d->x, w.rms_ffn, c.norm_eps, GK_GLU);
 	}
 	case 1:
@@ -1347,46 +1094,17 @@ static int enqueue_one_t(yalm_decoder_s *d, int kernel_id, int l) {
 		                   c.max_seq_len, d->part, d->attn_counters, nullptr, d->xb2, d->stream);
 	case 5:
 		return enqueue_logits_t<WT>(d);
-	case 7:
+	case 8: // fused attention + Wo
 		if constexpr (WT::BYTES <= 2)
-			return launch_ffn<WT>(d, w, l);
-		break;
-	case 8: // fused attention + Wo: granule hand-off form / short-context form
-	case 9:
-		if constexpr (WT::BYTES <= 2) {
-			const bool now = d->awo_local_now;
-			d->awo_local_now = kernel_id == 9;
-			const int r = launch_attn_wo<WT>(d, w, l);
-			d->awo_local_now = now;
-			return r;
-		}
+			return launch_attn_wo<WT>(d, w, l);
 		break;
 	}
 	set_err("bad kernel_id");
 	return YALM_ERR_ARG;
 }
 
-extern "C" int yalm_decoder_engine(yalm_decoder d) {
-	return d && d->engine ? 1 : 0;
-}
-
 extern "C" int yalm_decoder_attn_wo(yalm_decoder d) {
 	return d && d->attn_wo ? 1 : 0;
-}
-
-extern "C" int yalm_decoder_ffn(yalm_decoder d) {
-	return d && d->ffn ? 1 : 0;
-}
-
-extern "C" int yalm_ffn_trace(yalm_decoder d, unsigned long long *host, size_t count, int *workgroups) {
-	ARGCHK(d && host, "null argument");
-	ARGCHK(d->ffn && d->ffn_trace, "no ffn trace (create the decoder with YALM_FFN_TRACE=1)");
-	HIPCHK(hipStreamSynchronize(d->stream));
-	const size_t total = (size_t)FFN_TRACE_WORDS * d->ffn_nb;
-	HIPCHK(hipMemcpy(host, d->ffn_trace, sizeof(unsigned long long) * std::min(count, total), hipMemcpyDeviceToHost));
-	if (workgroups)
-		*workgroups = d->ffn_nb;
-	return YALM_OK;
 }
 
 extern "C" int yalm_attn_wo_trace(yalm_decoder d, unsigned long long *host, size_t count, int *workgroups,
@@ -1403,43 +1121,49 @@ extern "C" int yalm_attn_wo_trace(yalm_decoder d, unsigned long long *host, size
 	return YALM_OK;
 }
 
-extern "C" int yalm_time_kernel(yalm_decoder d, int kernel_id, int iters, float *avg_ms) {
-	ARGCHK(d && avg_ms && iters > 0 && kernel_id >= 0 && kernel_id <= 9, "bad argument");
-	ARGCHK(kernel_id < 8 || d->attn_wo, "kernels 8/9 (fused attention + Wo) need yalm_decoder_attn_wo");
-	ARGCHK(kernel_id != 9 || d->awo_local_max > 0, "kernel 9 (short-context attention + Wo) is disabled");
-	ARGCHK(kernel_id != 6 || d->engine, "kernel 6 (engine) needs a decoder running the persistent engine");
-	ARGCHK(kernel_id != 7 || d->ffn, "kernel 7 (fused feed-forward) needs a decoder with yalm_decoder_ffn");
+// Average ms per iteration of `iters` back-to-back enqueues of kernel_id on the
+// decoder stream (HIP events). With `bump`, every iteration first advances the step
+// epoch (one 1-thread kernel), so a fused attention + Wo launch sees fresh tags and
+// its Wo waves really wait for the heads (without it the granules of the
+// previous launch already match and the hand-off is not measured).
+static int time_loop(yalm_decoder_s *d, int kernel_id, int iters, bool bump, bool kernel, float *ms_out) {
 	hipEvent_t e0, e1;
 	HIPCHK(hipEventCreate(&e0));
 	HIPCHK(hipEventCreate(&e1));
-	if (kernel_id == 6) { // back-to-back greedy engine launches (each one token)
-		TRY(engine_enqueue(d, GRAPH_GREEDY));
-		HIPCHK(hipEventRecord(e0, d->stream));
-		for (int i = 0; i < iters; ++i)
-			TRY(engine_enqueue(d, GRAPH_GREEDY));
-		HIPCHK(hipEventRecord(e1, d->stream));
-		HIPCHK(hipEventSynchronize(e1));
-		TRY(engine_check(d));
-		float ms = 0.f;
-		HIPCHK(hipEventElapsedTime(&ms, e0, e1));
-		(void)hipEventDestroy(e0);
-		(void)hipEventDestroy(e1);
-		*avg_ms = ms / iters;
-		return YALM_OK;
-	}
-	// warm-up once, then time; rotate layers so weights come from HBM, not the
-	// 256 MiB Infinity Cache.
-	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_one_t, d, kernel_id, 0));
+	int r = YALM_OK;
 	HIPCHK(hipEventRecord(e0, d->stream));
-	for (int i = 0; i < iters; ++i)
-		TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_one_t, d, kernel_id, (i + 1) % d->c.n_layers));
+	for (int i = 0; i < iters && r == YALM_OK; ++i) {
+		if (bump)
+			epoch_bump_kernel<<<1, 1, 0, d->stream>>>(d->step);
+		// rotate layers so weights come from HBM, not the 256 MiB Infinity Cache
+		if (kernel)
+			r = DISPATCH_WT(d->c.weight_dtype, enqueue_one_t, d, kernel_id, (i + 1) % d->c.n_layers);
+	}
 	HIPCHK(hipEventRecord(e1, d->stream));
 	HIPCHK(hipEventSynchronize(e1));
 	float ms = 0.f;
 	HIPCHK(hipEventElapsedTime(&ms, e0, e1));
 	(void)hipEventDestroy(e0);
 	(void)hipEventDestroy(e1);
-	*avg_ms = ms / iters;
+	*ms_out = ms / iters;
+	return r;
+}
+
+extern "C" int yalm_time_kernel(yalm_decoder d, int kernel_id, int iters, float *avg_ms) {
+	ARGCHK(d && avg_ms && iters > 0 && kernel_id >= 0 && kernel_id <= 8 && kernel_id != 6 && kernel_id != 7,
+	       "bad argument (kernel ids 0-5, 8)");
+	ARGCHK(kernel_id != 8 || d->attn_wo, "kernel 8 (fused attention + Wo) needs yalm_decoder_attn_wo");
+	const bool bump = kernel_id == 8;
+	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_one_t, d, kernel_id, 0)); // warm-up
+	float ms = 0.f;
+	TRY(time_loop(d, kernel_id, iters, bump, true, &ms));
+	if (bump) { // minus the epoch bumps alone (one launch each), so one boundary per iteration stays in
+		float mb = 0.f;
+		TRY(time_loop(d, kernel_id, iters, true, false, &mb));
+		ms = std::max(0.f, ms - mb);
+	}
+	TRY(awo_check(d));
+	*avg_ms = ms;
 	return YALM_OK;
 }
 
@@ -1451,16 +1175,7 @@ extern "C" int yalm_set_gemv_config(yalm_decoder d, int kind, int threads, int u
 	d->gemv[kind] = GemvCfg{threads, unroll, gpw};
 	// captured graphs bake the old geometry: drop them
 	HIPCHK(hipStreamSynchronize(d->stream));
-	for (int v = 0; v < 2; ++v) {
-		for (int i = 0; i < N_GRAPHS; ++i) {
-			if (d->exec[v][i])
-				(void)hipGraphExecDestroy(d->exec[v][i]);
-			if (d->graph[v][i])
-				(void)hipGraphDestroy(d->graph[v][i]);
-			d->exec[v][i] = nullptr;
-			d->graph[v][i] = nullptr;
-		}
-	}
+	drop_graphs(d);
 	return YALM_OK;
 }
 
@@ -1468,37 +1183,27 @@ extern "C" const char *yalm_kernel_name(yalm_decoder d, int kernel_id) {
 	if (!d)
 		return "";
 	const char *wt = d->c.weight_dtype == YALM_F32 ? "WF32" : d->c.weight_dtype == YALM_F16 ? "WF16" : "WF8";
+	const std::string gk = std::string("gemv_rb_kernel<") + wt;
 	std::string s;
-	static const bool legacy = getenv("YALM_GEMV_LEGACY") && atoi(getenv("YALM_GEMV_LEGACY")) != 0;
-	const std::string gk = d->dyn ? "gemv_dyn_kernel<" : legacy ? "gemv_stream_kernel<" : "gemv_rb_kernel<";
 	switch (kernel_id) {
-	case 6:
-		s = std::string("engine_kernel<") + wt + ", ";
-		break;
 	case 0:
-		s = gk + wt + ", PQKV<";
+		s = gk + ", PQKV<";
 		break;
 	case 1:
 		s = "attn_decode_kernel<";
 		break;
 	case 2:
 	case 4:
-		s = gk + wt + ", PResidual<";
+		s = gk + ", PResidual<";
 		break;
 	case 3:
-		s = gk + wt + ", PGlu<";
+		s = gk + ", PGlu<";
 		break;
 	case 5:
-		s = gk + wt + ", PStore<";
-		break;
-	case 7:
-		s = std::string("ffn_kernel<") + wt + ", ";
+		s = gk + ", PStore<";
 		break;
 	case 8:
 		s = std::string("attn_wo_kernel<") + wt + ", ";
-		break;
-	case 9:
-		s = std::string("attn_wo_local_kernel<") + wt + ", ";
 		break;
 	default:
 		s = "";

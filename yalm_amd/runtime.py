@@ -104,13 +104,8 @@ _sig("yalm_get_logits", c_int, [c_void_p, c_void_p])
 _sig("yalm_time_kernel", c_int, [c_void_p, c_int, c_int, ctypes.POINTER(c_float)])
 _sig("yalm_kernel_name", ctypes.c_char_p, [c_void_p, c_int])
 _sig("yalm_set_gemv_config", c_int, [c_void_p, c_int, c_int, c_int, c_int])
-_sig("yalm_decoder_engine", c_int, [c_void_p])
 _sig("yalm_decoder_attn_wo", c_int, [c_void_p])
-_sig("yalm_decoder_ffn", c_int, [c_void_p])
-_sig("yalm_ffn_trace", c_int, [c_void_p, c_void_p, ctypes.c_size_t, ctypes.POINTER(c_int)])
 _sig("yalm_attn_wo_trace", c_int, [c_void_p, c_void_p, ctypes.c_size_t, ctypes.POINTER(c_int), ctypes.POINTER(c_int)])
-_sig("yalm_attn_wo_local_trace", c_int, [c_void_p, c_void_p, ctypes.c_size_t, ctypes.POINTER(c_int)])
-_sig("yalm_engine_trace", c_int, [c_void_p, c_void_p, ctypes.c_size_t, ctypes.POINTER(c_int)])
 _sig("yalm_matmul", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int])
 _sig("yalm_mha", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int])
 _sig("yalm_ffn", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int])
@@ -132,8 +127,7 @@ EXPORTED = [
     "yalm_time_kernel", "yalm_kernel_name", "yalm_set_gemv_config", "yalm_matmul", "yalm_mha", "yalm_ffn",
     "yalm_prefill", "yalm_prefill_time", "yalm_gemm_f16", "yalm_attn_prefill", "yalm_tp_unique_id",
     "yalm_decoder_create_tp", "yalm_copy_2d", "yalm_tp_ipc_alloc", "yalm_decoder_create_tp_ipc",
-    "yalm_decoder_engine", "yalm_engine_trace", "yalm_decoder_attn_wo", "yalm_attn_wo_trace", "yalm_attn_wo_local_trace",
-    "yalm_decoder_ffn", "yalm_ffn_trace",
+    "yalm_decoder_attn_wo", "yalm_attn_wo_trace",
 ]
 
 HYDRATE_KV_CACHE, OUTPUT_LOGITS = 0, 1
@@ -425,11 +419,6 @@ class Decoder:
         check(lib.yalm_set_gemv_config(self.h, kind, threads, unroll, gpw))
 
     @property
-    def engine(self) -> bool:
-        """True when each token runs as one persistent engine launch (engine.h)."""
-        return bool(lib.yalm_decoder_engine(self.h))
-
-    @property
     def attn_wo(self) -> bool:
         """True when the launch path runs attention + Wo as one launch (attn_wo.h)."""
         return bool(lib.yalm_decoder_attn_wo(self.h))
@@ -441,36 +430,6 @@ class Decoder:
         nb, na = c_int(), c_int()
         check(lib.yalm_attn_wo_trace(self.h, buf.ctypes.data, buf.size, ctypes.byref(nb), ctypes.byref(na)))
         return buf[: 4 * nb.value].reshape(nb.value, 4), na.value
-
-    def attn_wo_local_trace(self) -> np.ndarray:
-        """(workgroups, 4) uint64 stamps of the last short-context attention + Wo
-        launch (attn_wo_local_kernel; decoder created with YALM_ATTN_WO_TRACE=1)."""
-        buf = np.zeros(4 * 8192, np.uint64)
-        nb = c_int()
-        check(lib.yalm_attn_wo_local_trace(self.h, buf.ctypes.data, buf.size, ctypes.byref(nb)))
-        return buf[: 4 * nb.value].reshape(nb.value, 4)
-
-    @property
-    def ffn(self) -> bool:
-        """True when the launch path runs rmsnorm + GLU + W2 + residual as one launch (ffn.h)."""
-        return bool(lib.yalm_decoder_ffn(self.h))
-
-    def ffn_trace(self) -> np.ndarray:
-        """(workgroups, 8) uint64 stamps of the last fused feed-forward launch
-        (decoder created with YALM_FFN_TRACE=1); see yalm_ffn_trace."""
-        buf = np.zeros(8 * 4096, np.uint64)
-        nb = c_int()
-        check(lib.yalm_ffn_trace(self.h, buf.ctypes.data, buf.size, ctypes.byref(nb)))
-        return buf[: 8 * nb.value].reshape(nb.value, 8)
-
-    def engine_trace(self) -> np.ndarray:
-        """(workgroups, 5 L + 2, 8) uint64 timeline of the last engine launch
-        (decoder created with YALM_ENGINE_TRACE=1); see yalm_engine_trace."""
-        e = 5 * self.cfg.n_layers + 2
-        buf = np.zeros(1024 * e * 8, np.uint64)
-        nb = c_int()
-        check(lib.yalm_engine_trace(self.h, buf.ctypes.data, buf.size, ctypes.byref(nb)))
-        return buf[: nb.value * e * 8].reshape(nb.value, e, 8)
 
     def kernel_name(self, kernel_id: int) -> str:
         return lib.yalm_kernel_name(self.h, kernel_id).decode()
