@@ -1,21 +1,28 @@
 """Decode benchmark — BASELINE.json metric "decode tok/s Mistral-7B fp16 @1 GPU;
-% of HBM bytes/token roofline" on config 2 (Mistral-7B fp16, 1x MI355X,
-greedy -t 0, 256 tokens).
+% of HBM bytes/token roofline".
 
-A step = one decode token: the whole per-token forward (embedding, 32
-blocks, final norm, logits GEMV, device argmax feeding the next token) as one
-hipGraph replay. Weights are random (no checkpoints offline) but of the real
+N = 1: config 2 (Mistral-7B fp16, 1x MI355X, greedy -t 0); `--dtype fp8` is
+config 3 (E5M2 weights). N > 1: config 5, one sequence tensor-parallel over N
+GPUs (Megatron split, RCCL all-reduce captured in the per-token graph);
+`--replicas` runs N independent decoders instead, `--tp-transport ipc` the IPC
+one-shot exchange.
+
+A step = one decode token: the whole per-token forward (embedding, 32 blocks,
+final norm, logits GEMV, device argmax feeding the next token) as one hipGraph
+replay. Weights are random (no checkpoints offline) but of the real
 architecture and size, generated in HBM before timing. The prompt is 13
 synthetic token ids (the README prompt's length) hydrated first.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype fp16|fp8]
-For N>1 launch under torch.distributed.run: each rank decodes its own
-sequence on its GPU (replicas; no collective on the data path) and rank 0
-reports total tokens / max-over-ranks time.
+With --gpus N > 1 and no WORLD_SIZE in the environment, the script starts N
+rank processes itself (before any GPU call); under torch.distributed.run each
+rank reads RANK / LOCAL_RANK / WORLD_SIZE. Rank 0 prints ONE JSON line.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -36,25 +43,70 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample budget")
     ap.add_argument("--kernel-iters", type=int, default=64)
-    ap.add_argument("--tp", action="store_true",
-                    help="tensor parallel over the launched ranks (one sequence) instead of replicas")
+    ap.add_argument("--replicas", action="store_true",
+                    help="N > 1: N independent decoders (one sequence per GPU) instead of tensor parallelism")
+    ap.add_argument("--tp", action="store_true", help="tensor parallel even at N = 1 (TP1 through the transport)")
     ap.add_argument("--tp-transport", default="rccl", choices=["rccl", "ipc"],
-                    help="all-reduce transport for --tp: RCCL (one rank per GPU) or the IPC one-shot exchange")
+                    help="all-reduce transport for tensor parallelism: RCCL (one rank per GPU) or the IPC one-shot exchange")
+    ap.add_argument("--no-envelope", action="store_true")
     return ap.parse_args()
 
 
-def pmc_traffic(kernel_match, dtype):
+def spawn_ranks(n):
+    """--gpus N without a launcher: start N copies of this script as ranks 0..N-1
+    (each picks GPU LOCAL_RANK) and return the worst exit code. Nothing here has
+    touched the GPU."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return max(rcs, key=abs)
+
+
+def gpu_state():
+    """Clocks and partition modes as rocm-smi reports them (a separate process;
+    the box's own state explains box-to-box spread)."""
+    out = {}
+    try:
+        r = subprocess.run(["rocm-smi", "--showclocks", "--showcomputepartition", "--showmemorypartition", "--json"],
+                           capture_output=True, text=True, timeout=30)
+        d = json.loads(r.stdout)
+        card = d[sorted(d)[0]] if d else {}
+        for k, v in card.items():
+            kl = k.lower()
+            if "sclk" in kl or "mclk" in kl or "fclk" in kl or "partition" in kl:
+                out[k] = v
+    except Exception as e:  # report, never fail the bench on it
+        out["error"] = repr(e)[:200]
+    return out
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def pmc_traffic(kernel_match):
     """HBM bytes per launch of the dominant kernel from the newest committed
     rocprofv3 --pmc FETCH_SIZE pass that profiled it (profiles/*_pmc_fetch_size*.csv):
     median FETCH_SIZE (KB) x 1024 x 2 -- gfx950 counts half the bytes of 16 B/lane
     streaming reads (MI355X_MICROARCH.md §HBM). `kernel_match`: substrings that
-    must all appear in the kernel name. None if no matching profile."""
+    must all appear in the kernel name (the weight type is part of it, so fp16 and
+    fp8 passes never mix). None if no matching profile."""
     import csv
     import glob
     import statistics
 
-    if dtype != "fp16":
-        return None, None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_fetch_size*.csv")), reverse=True):
         rows = list(csv.DictReader(open(f)))
         vals = [float(r["Counter_Value"]) for r in rows
@@ -67,18 +119,30 @@ def pmc_traffic(kernel_match, dtype):
 def cpu_baseline(cfg, budget_s):
     """The CPU oracle (oracle/, restatement of the reference -d cpu path with
     its AVX2/F16C GEMV and OpenMP) on the same synthetic weights, timed on
-    this host. Bounded sample: hydrate the prompt, then decode until the
-    budget is spent (at least 2 tokens)."""
+    this host. Thread count: nproc (BASELINE.md CPU-baseline plan) and the
+    OMP_NUM_THREADS share the harness sets are both probed on a few tokens and
+    the faster one runs the bounded sample (hydrate the prompt, then decode
+    until the budget is spent, at least 2 tokens)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import numpy as np
 
     import oracle_py as O
 
-    threads = int(os.environ.get("YALM_CPU_THREADS", min(16, os.cpu_count() or 1)))
-    O.set_threads(threads)
+    nproc = len(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    cands = sorted({c for c in (nproc, share) if c > 0})
     host = O.synth_host_tensors_fast(cfg, seed=1)
     om = O.OracleModel(cfg, host)
     prompt = [(7 * i + 1) % cfg.vocab_size for i in range(PROMPT_LEN)]
+    probe = {}
+    for th in cands:  # hydrate the prompt with each candidate (identical work), time it
+        O.set_threads(th)
+        t0 = time.perf_counter()
+        for pos, t in enumerate(prompt[:4]):
+            om.forward(t, pos, 0)
+        probe[th] = 4 / (time.perf_counter() - t0)
+    threads = max(probe, key=probe.get)
+    O.set_threads(threads)
     for pos, t in enumerate(prompt):
         om.forward(t, pos, 1 if pos == len(prompt) - 1 else 0)
     tok = int(np.argmax(om.buf["logits"]))
@@ -97,66 +161,104 @@ def cpu_baseline(cfg, budget_s):
         "unit": "tok/s",
         "cores": threads,
         "kind": "port",
+        "cpu_model": cpu_model(),
+        "nproc": nproc,
         "sample": f"oracle -d cpu restatement, {n} greedy decode tokens after a {PROMPT_LEN}-token prompt, "
                   f"same synthetic Mistral-7B {'fp16' if cfg.weight_dtype == 1 else 'fp8'} weights, "
-                  f"{threads} OpenMP threads, {el:.1f} s",
+                  f"{threads} OpenMP threads ({el:.1f} s); thread probe tok/s "
+                  + ", ".join(f"{k}: {v:.2f}" for k, v in sorted(probe.items())),
     }
+
+
+def tp_bytes_per_token(cfg, size):
+    """Algorithmic HBM bytes ONE rank reads per token under the Megatron split
+    (include/yalm_hip.h): 1/size of every sharded matrix and of the classifier,
+    the replicated norms and embedding row."""
+    from yalm_amd import models as M
+
+    wb = M.DTYPE_BYTES[cfg.weight_dtype]
+    per_layer = 2 * cfg.dim * 4
+    per_layer += (cfg.q_dim + 2 * cfg.kv_dim) // size * cfg.dim * wb
+    per_layer += cfg.dim * cfg.q_dim // size * wb
+    per_layer += 3 * cfg.dim * cfg.hidden_dim // size * wb
+    return cfg.n_layers * per_layer + cfg.dim * wb + cfg.dim * 4 + cfg.vocab_size // size * cfg.dim * wb
+
+
+def make_decoder(runtime, M, cfg, rank, world, mode, dist):
+    """(DeviceModel, Decoder) for mode "single" | "replica" | "tp-rccl" | "tp-ipc"."""
+    if mode in ("single", "replica"):
+        dm = runtime.DeviceModel.synthetic(cfg, seed=1)
+        return dm, runtime.Decoder(dm)
+    dm = runtime.DeviceModel.synthetic(cfg, seed=1, tp=(rank, world))
+    if mode == "tp-ipc":
+        def gather(h):
+            out = [None] * world
+            dist.all_gather_object(out, h)
+            return out
+
+        return dm, runtime.Decoder(dm, tp_gather=gather if world > 1 else (lambda h: [h]))
+    uid = [runtime.tp_unique_id() if rank == 0 else None]
+    if world > 1:
+        dist.broadcast_object_list(uid, src=0)
+    return dm, runtime.Decoder(dm, tp_id=uid[0])
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    dev = local_rank
     if world > 1:
-        import torch
         import torch.distributed as dist_mod
 
-        # one rank per GPU; more ranks than GPUs (a 1-GPU rehearsal of the N > 1
-        # path) share devices round-robin
-        dev = local_rank % max(1, torch.cuda.device_count())
-        torch.cuda.set_device(dev)
-        if torch.cuda.device_count() >= world:
-            dist_mod.init_process_group("nccl", device_id=torch.device("cuda", dev))
-        else:
-            dist_mod.init_process_group("gloo")
+        # host-side control only (unique id, barriers, max-over-ranks time): gloo;
+        # the data path is the decoder's own RCCL communicator / IPC exchange
+        dist_mod.init_process_group("gloo")
         dist = dist_mod
 
+    state = gpu_state() if local_rank == 0 else None
     from yalm_amd import models as M
     from yalm_amd import runtime
 
+    ndev = int(os.environ.get("YALM_BENCH_NDEV", "0")) or None
+    dev = local_rank if ndev is None else local_rank % ndev
     runtime.check(runtime.lib.yalm_set_device(dev))
     base = M.PRESETS[args.model]
     cfg = base.with_(weight_dtype=M.F16 if args.dtype == "fp16" else M.F8E5M2)
 
-    if args.tp:
-        # one sequence sharded over all ranks (Megatron split, RCCL all-reduce in the graph)
-        dm = runtime.DeviceModel.synthetic(cfg, seed=1, tp=(rank, world))
-        if args.tp_transport == "ipc":
-            def gather(h):
-                if dist is None:
-                    return [h]
-                out = [None] * world
-                dist.all_gather_object(out, h)
-                return out
-
-            dec = runtime.Decoder(dm, tp_gather=gather)
-        else:
-            uid = [runtime.tp_unique_id() if rank == 0 else None]
-            if dist is not None:
-                dist.broadcast_object_list(uid, src=0)
-            dec = runtime.Decoder(dm, tp_id=uid[0])
+    if world == 1:
+        mode = f"tp-{args.tp_transport}" if args.tp else "single"
     else:
-        dm = runtime.DeviceModel.synthetic(cfg, seed=1)
-        dec = runtime.Decoder(dm)
+        mode = "replica" if args.replicas else f"tp-{args.tp_transport}"
+    fallback = None
+    try:
+        dm, dec = make_decoder(runtime, M, cfg, rank, world, mode, dist)
+        ok = 1
+    except Exception as e:  # a transport that cannot come up on this node: say so, then fall back
+        fallback = f"{mode} failed on rank {rank}: {str(e)[:200]}"
+        ok = 0
+    if dist is not None:
+        oks = [None] * world
+        dist.all_gather_object(oks, ok)
+        if not all(oks) and ok:
+            dec.close()
+            dm.close()
+            fallback = fallback or f"{mode} failed on another rank"
+            ok = 0
+    if not ok:
+        mode = "replica" if world > 1 else "single"
+        dm, dec = make_decoder(runtime, M, cfg, rank, world, mode, dist)
+    tp = mode.startswith("tp-")
+    tp_size = world if tp else 1
+
     prompt = [(7 * i + 1) % cfg.vocab_size for i in range(PROMPT_LEN)]
     for pos, t in enumerate(prompt[:-1]):
         dec.forward(t, pos, runtime.HYDRATE_KV_CACHE)
     # first generated token; the device loop continues from there
-    first = dec.generate_greedy(prompt[-1], PROMPT_LEN - 1, 1)[0]
-    del first
+    dec.generate_greedy(prompt[-1], PROMPT_LEN - 1, 1)
     if args.warmup:
         dec.enqueue_greedy(args.warmup)
     runtime.check(runtime.lib.yalm_stream_sync(None))
@@ -166,9 +268,6 @@ def main():
         runtime.check(runtime.lib.yalm_stream_sync(None))
         dec.device_step()  # syncs the decoder stream
         if dist is not None:
-            import torch
-
-            torch.cuda.synchronize()
             dist.barrier()
 
     barrier_sync()
@@ -178,43 +277,45 @@ def main():
     t1 = time.perf_counter()
     barrier_sync()
     elapsed = t1 - t0
-    if dist is not None:
-        import torch
-
-        tt = torch.tensor([elapsed], dtype=torch.float64,
-                          device="cuda" if dist.get_backend() == "nccl" else "cpu")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-    _, pos1 = dec.device_step()
+    tok1, pos1 = dec.device_step()
     assert pos1 - pos0 == args.steps, (pos0, pos1)
+    agree = None
+    if dist is not None:
+        allv = [None] * world
+        dist.all_gather_object(allv, (elapsed, tok1))
+        elapsed = max(v[0] for v in allv)
+        if tp:  # every rank must have produced the same token sequence
+            agree = len({v[1] for v in allv}) == 1
 
-    # ---- roofline of the dominant kernel: the fused feed-forward launch (rmsnorm +
-    # W1/W3 + GLU + W2 + residual, 79.3% of the bytes) when the decoder runs it, else
-    # the W1/W3 GEMV + SiLU-GLU (52.9% of the bytes)
+    # ---- roofline of the dominant kernel: the W1/W3 GEMV + SiLU-GLU (52.9% of the bytes)
     wb = M.DTYPE_BYTES[cfg.weight_dtype]
-    hid_local = cfg.hidden_dim // (world if args.tp else 1)
-    if dec.ffn:
-        KID = 7
-        # W1, W3, W2 + rms_ffn + x read + x rows written + hb written once
-        kern_bytes = 3 * hid_local * cfg.dim * wb + 3 * cfg.dim * 4 + hid_local * 4
-        match = ("ffn_kernel<WF16",)
-    else:
-        KID = 3
-        kern_bytes = 2 * hid_local * cfg.dim * wb + 2 * cfg.dim * 4 + hid_local * 4
-        match = ("gemv_rb_kernel<WF16", "PGlu")
+    hid_local = cfg.hidden_dim // tp_size
+    KID = 3
+    kern_bytes = 2 * hid_local * cfg.dim * wb + 2 * cfg.dim * 4 + hid_local * 4
+    wt = "WF16" if args.dtype == "fp16" else "WF8"
     avg_ms = dec.time_kernel(KID, args.kernel_iters)
     achieved = kern_bytes / (avg_ms * 1e-3) / 1e9
     kname = dec.kernel_name(KID)
-    traffic, traffic_src = pmc_traffic(match, args.dtype)
+    traffic, traffic_src = pmc_traffic((f"gemv_rb_kernel<{wt}", "PGlu"))
+    exch_us = None
+    if tp and tp_size > 1:
+        exch_us = dec.time_kernel(6, args.kernel_iters) * 1e3
+    env_ms = None
+    if not args.no_envelope:
+        if dist is not None:
+            dist.barrier()
+        env_ms = runtime.stream_envelope(kern_bytes, 16)
 
-    toks = args.steps * (1 if args.tp else world)
+    toks = args.steps * (1 if tp else world)
     value = toks / elapsed
     kv_avg = (pos0 + pos1) / 2 + 1
+    n_seq = 1 if tp else world
+    if tp:
+        rank_bytes = tp_bytes_per_token(cfg, tp_size) + cfg.kv_bytes_per_token(int(kv_avg)) // tp_size
+    else:
+        rank_bytes = cfg.weight_bytes_per_token() + cfg.kv_bytes_per_token(int(kv_avg))
+    per_gpu_gbs = rank_bytes * (args.steps / elapsed) / 1e9
     bytes_per_tok = cfg.weight_bytes_per_token() + cfg.kv_bytes_per_token(int(kv_avg))
-    step_gbs = bytes_per_tok * (args.steps / elapsed) / 1e9  # per sequence
-    n_seq = 1 if args.tp else world
-    agg_gbs = step_gbs * n_seq  # all GPUs
-    peak_all = HBM_PEAK_GBS * world
 
     out = {
         "metric": "decode tok/s Mistral-7B fp16 @1 GPU; % of HBM bytes/token roofline"
@@ -226,27 +327,27 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "strong" if args.tp else "weak",
+        "scaling": "strong" if tp else "weak",
         "vs_baseline": None,
         "dtype": "f16" if args.dtype == "fp16" else "f8e5m2",
         "data": "synthetic (random weights of the real Mistral-7B-v0.2 shape generated in HBM; "
                 f"{PROMPT_LEN}-token synthetic prompt; greedy argmax on device)",
         "config": {
             "workload": f"{args.model} {args.dtype} batch-1 greedy decode, {args.steps} tokens"
-                        f"{' (one sequence, tensor parallel)' if args.tp else '/GPU'}, "
-                        f"kv_len {pos0 + 1}..{pos1}",
+                        f"{f' (one sequence, tensor parallel over {world} GPUs)' if tp and world > 1 else ''}"
+                        f"{'/GPU' if not tp and world > 1 else ''}, kv_len {pos0 + 1}..{pos1}",
             "model": args.model,
-            "global_batch": world,
+            "global_batch": n_seq,
             "seq_len": int(pos1),
-            "parallelism": (f"tp{world}-{args.tp_transport}" if args.tp else
-                            (f"replicas{world}" if world > 1 else "single")),
+            "parallelism": (f"tp{tp_size}-{mode[3:]}" if tp else (f"replicas{world}" if world > 1 else "single")),
         },
         "step_roofline": {
             "bytes_per_token": int(bytes_per_tok),
-            "achieved": round(agg_gbs, 1),
-            "peak": peak_all,
+            "bytes_per_token_per_gpu": int(rank_bytes),
+            "achieved_per_gpu": round(per_gpu_gbs, 1),
+            "peak_per_gpu": HBM_PEAK_GBS,
             "unit": "GB/s",
-            "frac": round(agg_gbs / peak_all, 4),
+            "frac": round(per_gpu_gbs / HBM_PEAK_GBS, 4),
         },
         "roofline": {
             "bound": "hbm",
@@ -259,9 +360,22 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
             "traffic_source": traffic_src,
+            "envelope_us": round(env_ms * 1e3, 3) if env_ms else None,
+            "envelope_gbs": round(kern_bytes / (env_ms * 1e-3) / 1e9, 1) if env_ms else None,
+            "frac_of_envelope": round(env_ms / avg_ms, 4) if env_ms else None,
         },
+        "gpu_state": state,
         "cpu_baseline": None,
     }
+    if tp and tp_size > 1:
+        out["tp"] = {
+            "exchange_us": round(exch_us, 3),
+            "exchanges_per_token": 2 * cfg.n_layers + 1,
+            "exchange_ms_per_token": round(exch_us * (2 * cfg.n_layers + 1) / 1e3, 4),
+            "ranks_agree": agree,
+        }
+    if fallback:
+        out["fallback"] = fallback
     dec.close()
     dm.close()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -274,6 +388,8 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    if agree is False:
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -135,12 +135,20 @@ int yalm_get_logits(yalm_decoder d, float *host);
 /* Average device time (ms) of one kernel of the forward, launched eagerly on
  * the decoder's stream `iters` times between HIP events (layers rotated so the
  * weights come from HBM). kernel_id: 0 = QKV GEMV, 1 = attention, 2 = Wo GEMV,
- * 3 = W1/W3 GEMV+GLU, 4 = W2 GEMV, 5 = logits GEMV, 8 = the fused attention + Wo
+ * 3 = W1/W3 GEMV+GLU, 4 = W2 GEMV, 5 = logits GEMV, 6 = one tensor-parallel
+ * exchange of x (RCCL all-reduce or IPC exchange; collective: every rank calls it
+ * with the same iters), 8 = the fused attention + Wo
  * launch (yalm_decoder_attn_wo; each timed launch gets a fresh step epoch, so its
  * Wo waves wait for the heads as in a real forward; the epoch-bump launches are
  * timed separately and subtracted). Used by bench.py for the roofline of the
  * dominant kernel. */
 int yalm_time_kernel(yalm_decoder d, int kernel_id, int iters, float *avg_ms);
+/* The same-process streaming envelope: average ms of one pure read-only pass over
+ * `bytes` of HBM (16-byte non-temporal loads, the best of a few wave geometries,
+ * `iters` back-to-back launches alternating two buffers so the 256 MiB Infinity
+ * Cache cannot serve them). bench.py reports a kernel's time against it so the
+ * roofline fraction is also stated relative to what THIS box streams. */
+int yalm_stream_envelope(size_t bytes, int iters, float *avg_ms);
 /* Override the GEMV launch geometry of one weight-streaming kernel kind
  * (0 = QKV, 1 = Wo, 2 = W1/W3, 3 = W2, 4 = logits): workgroup size
  * 256|512|1024, unroll (16-byte loads in flight per lane) 2|4|8, and `gpw` =

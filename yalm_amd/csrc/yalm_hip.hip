@@ -431,6 +431,26 @@ static const unsigned *ipc_seq(const yalm_decoder_s *d) {
 	return (const unsigned *)(d->ipc_own + 2 * (size_t)d->ipc_S) + 64;
 }
 
+// One tensor-parallel exchange of x alone (the all-reduce that follows the Wo / W2
+// partials): timing hook for the per-token communication cost (yalm_time_kernel id 6).
+static int enqueue_exchange(yalm_decoder_s *d) {
+	if (d->ipc) {
+		ipc_exchange_kernel<<<1, 1024, 0, d->stream>>>(d->ipc_bufs, d->tp_rank, d->tp_size, d->ipc_S, 0, d->c.dim,
+		                                              IPC_SUM, d->xs);
+		HIPCHK(hipGetLastError());
+		return YALM_OK;
+	}
+	if (!d->comm) {
+		set_err("kernel 6 (tensor-parallel exchange) needs a tensor-parallel decoder");
+		return YALM_ERR_ARG;
+	}
+	if (ncclAllReduce(d->x, d->xs, d->c.dim, ncclFloat, ncclSum, (ncclComm_t)d->comm, d->stream) != ncclSuccess) {
+		set_err("ncclAllReduce failed");
+		return YALM_ERR_HIP;
+	}
+	return YALM_OK;
+}
+
 // x += W v (fused_matmul_add_residuals). Under tensor parallelism W holds this
 // rank's input columns: rank 0 writes xs = x + W v, the others xs = W v, and
 // one RCCL all-reduce (sum, captured in the graph) lands x + sum_r W_r v_r in x
@@ -1094,6 +1114,8 @@ static int enqueue_one_t(yalm_decoder_s *d, int kernel_id, int l) {
 		                   c.max_seq_len, d->part, d->attn_counters, nullptr, d->xb2, d->stream);
 	case 5:
 		return enqueue_logits_t<WT>(d);
+	case 6:
+		return enqueue_exchange(d);
 	case 8: // fused attention + Wo
 		if constexpr (WT::BYTES <= 2)
 			return launch_attn_wo<WT>(d, w, l);
@@ -1150,8 +1172,9 @@ static int time_loop(yalm_decoder_s *d, int kernel_id, int iters, bool bump, boo
 }
 
 extern "C" int yalm_time_kernel(yalm_decoder d, int kernel_id, int iters, float *avg_ms) {
-	ARGCHK(d && avg_ms && iters > 0 && kernel_id >= 0 && kernel_id <= 8 && kernel_id != 6 && kernel_id != 7,
-	       "bad argument (kernel ids 0-5, 8)");
+	ARGCHK(d && avg_ms && iters > 0 && kernel_id >= 0 && kernel_id <= 8 && kernel_id != 7,
+	       "bad argument (kernel ids 0-6, 8)");
+	ARGCHK(kernel_id != 6 || d->comm || d->ipc, "kernel 6 (tensor-parallel exchange) needs a tensor-parallel decoder");
 	ARGCHK(kernel_id != 8 || d->attn_wo, "kernel 8 (fused attention + Wo) needs yalm_decoder_attn_wo");
 	const bool bump = kernel_id == 8;
 	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_one_t, d, kernel_id, 0)); // warm-up
@@ -1202,6 +1225,9 @@ extern "C" const char *yalm_kernel_name(yalm_decoder d, int kernel_id) {
 	case 5:
 		s = gk + ", PStore<";
 		break;
+	case 6:
+		s = d->ipc ? "ipc_exchange_kernel" : d->comm ? "AllReduce" : "";
+		break;
 	case 8:
 		s = std::string("attn_wo_kernel<") + wt + ", ";
 		break;
@@ -1210,6 +1236,94 @@ extern "C" const char *yalm_kernel_name(yalm_decoder d, int kernel_id) {
 	}
 	d->kname = s;
 	return d->kname.c_str();
+}
+
+namespace {
+struct DevBufT {
+	void *p = nullptr;
+	~DevBufT() {
+		if (p)
+			(void)hipFree(p);
+	}
+};
+} // namespace
+
+// ------------------------------------------------------------------ streaming envelope
+// Pure read-only HBM stream (tools/stream_bench.hip): each wave sums `per_wave`
+// contiguous 16-byte pieces with U nt loads in flight per lane; the result is
+// consumed only to keep the loads alive.
+template <int U>
+__global__ __launch_bounds__(512) void stream_read_kernel(const u32x4_t *__restrict__ p, size_t n16, size_t per_wave,
+                                                          unsigned *out) {
+	const size_t wave = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) / 64;
+	const int lane = threadIdx.x & 63;
+	const size_t base = wave * per_wave;
+	const size_t end = base + per_wave < n16 ? base + per_wave : n16;
+	unsigned acc = 0;
+	for (size_t i = base + lane; i < end; i += 64 * U) {
+		u32x4_t v[U];
+#pragma unroll
+		for (int u = 0; u < U; ++u) {
+			const size_t j = i + (size_t)u * 64;
+			v[u] = j < end ? load_nt16(p + j) : u32x4_t{0u, 0u, 0u, 0u};
+		}
+#pragma unroll
+		for (int u = 0; u < U; ++u)
+			acc ^= v[u][0] ^ v[u][1] ^ v[u][2] ^ v[u][3];
+	}
+	if (acc == 0x12345678u)
+		out[0] = acc;
+}
+
+extern "C" int yalm_stream_envelope(size_t bytes, int iters, float *avg_ms) {
+	ARGCHK(avg_ms && iters > 0 && bytes >= (1u << 20), "yalm_stream_envelope: bad argument");
+	bytes &= ~(size_t)4095;
+	DevBufT buf[2];
+	unsigned *out = nullptr;
+	for (auto &b : buf) {
+		HIPCHK(hipMalloc(&b.p, bytes));
+		HIPCHK(hipMemset(b.p, 1, bytes));
+	}
+	HIPCHK(hipMalloc((void **)&out, 64));
+	hipEvent_t e0, e1;
+	HIPCHK(hipEventCreate(&e0));
+	HIPCHK(hipEventCreate(&e1));
+	float best = 1e30f;
+	const size_t n16 = bytes / 16;
+	int r = YALM_OK;
+	for (size_t pw_bytes : {16384ul, 32768ul, 65536ul}) {
+		for (int U : {4, 8}) {
+			const size_t per_wave = pw_bytes / 16;
+			const size_t waves = (n16 + per_wave - 1) / per_wave;
+			const int blocks = (int)((waves + 7) / 8);
+			for (int pass = 0; pass < 2 && r == YALM_OK; ++pass) { // pass 0 warms up
+				if (hipEventRecord(e0, nullptr) != hipSuccess)
+					r = YALM_ERR_HIP;
+				for (int it = 0; it < iters && r == YALM_OK; ++it) { // alternate buffers: 2x bytes > 256 MiB MALL
+					const u32x4_t *src = (const u32x4_t *)buf[it & 1].p;
+					if (U == 4)
+						stream_read_kernel<4><<<blocks, 512>>>(src, n16, per_wave, out);
+					else
+						stream_read_kernel<8><<<blocks, 512>>>(src, n16, per_wave, out);
+				}
+				float ms = 0.f;
+				if (r == YALM_OK && (hipEventRecord(e1, nullptr) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+				                     hipEventElapsedTime(&ms, e0, e1) != hipSuccess))
+					r = YALM_ERR_HIP;
+				if (pass == 1 && r == YALM_OK)
+					best = std::min(best, ms / iters);
+			}
+		}
+	}
+	(void)hipEventDestroy(e0);
+	(void)hipEventDestroy(e1);
+	(void)hipFree(out);
+	if (r != YALM_OK) {
+		set_err("yalm_stream_envelope: HIP call failed");
+		return r;
+	}
+	*avg_ms = best;
+	return YALM_OK;
 }
 
 // ------------------------------------------------------------------ test API (host pointers)

@@ -104,6 +104,7 @@ _sig("yalm_get_logits", c_int, [c_void_p, c_void_p])
 _sig("yalm_time_kernel", c_int, [c_void_p, c_int, c_int, ctypes.POINTER(c_float)])
 _sig("yalm_kernel_name", ctypes.c_char_p, [c_void_p, c_int])
 _sig("yalm_set_gemv_config", c_int, [c_void_p, c_int, c_int, c_int, c_int])
+_sig("yalm_stream_envelope", c_int, [ctypes.c_size_t, c_int, ctypes.POINTER(c_float)])
 _sig("yalm_decoder_attn_wo", c_int, [c_void_p])
 _sig("yalm_attn_wo_trace", c_int, [c_void_p, c_void_p, ctypes.c_size_t, ctypes.POINTER(c_int), ctypes.POINTER(c_int)])
 _sig("yalm_matmul", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int])
@@ -127,7 +128,7 @@ EXPORTED = [
     "yalm_time_kernel", "yalm_kernel_name", "yalm_set_gemv_config", "yalm_matmul", "yalm_mha", "yalm_ffn",
     "yalm_prefill", "yalm_prefill_time", "yalm_gemm_f16", "yalm_attn_prefill", "yalm_tp_unique_id",
     "yalm_decoder_create_tp", "yalm_copy_2d", "yalm_tp_ipc_alloc", "yalm_decoder_create_tp_ipc",
-    "yalm_decoder_attn_wo", "yalm_attn_wo_trace",
+    "yalm_decoder_attn_wo", "yalm_attn_wo_trace", "yalm_stream_envelope",
 ]
 
 HYDRATE_KV_CACHE, OUTPUT_LOGITS = 0, 1
@@ -178,6 +179,13 @@ def ffn(x, w1, w2, w3, act: int, dtype: int) -> np.ndarray:
     out = np.zeros(dim, np.float32)
     check(lib.yalm_ffn(_ptr(out), _ptr(x), _ptr(w1), _ptr(w2), _ptr(w3), hidden_dim, dim, act, dtype))
     return out
+
+
+def stream_envelope(nbytes: int, iters: int = 16) -> float:
+    """ms of one pure HBM read pass over nbytes (yalm_stream_envelope)."""
+    ms = c_float()
+    check(lib.yalm_stream_envelope(nbytes, iters, ctypes.byref(ms)))
+    return ms.value
 
 
 def tp_unique_id() -> bytes:
