@@ -239,6 +239,13 @@ int yalm_mha(float *xout, float *att, const uint16_t *kb, const uint16_t *vb, co
 int yalm_ffn(float *xout, const float *x, const void *w1, const void *w2, const void *w3, int hidden_dim, int dim,
              int act, int dtype);
 
+/* Device greedy sampling (sampler.cpp:27-38 sample_argmax: strict '>' scan, the
+ * FIRST maximum wins, 0 when nothing exceeds -FLT_MAX): *out = argmax of n host
+ * logits through argmax_kernel, the kernel of the -t 0 decode loop. n_shards > 1
+ * runs the tensor-parallel form instead: one per-shard first max as a (value,
+ * global index) pair over each n / n_shards slice, then argmax_pick_kernel. */
+int yalm_argmax(const float *logits, int n, int n_shards, int *out);
+
 /* Prefill building blocks (host pointers, synchronous):
  * c[M][N] f32 = a[M][K] f16 · w[N][K]^T f16 (the MFMA GEMM; N % 128 == 0, K % 64 == 0). */
 int yalm_gemm_f16(float *c, const uint16_t *a, const uint16_t *w, int M, int N, int K);

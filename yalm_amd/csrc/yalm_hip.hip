@@ -1402,6 +1402,30 @@ extern "C" int yalm_mha(float *xout, float *att, const uint16_t *kb, const uint1
 	return YALM_OK;
 }
 
+extern "C" int yalm_argmax(const float *logits, int n, int n_shards, int *out) {
+	ARGCHK(logits && out && n > 0 && n_shards >= 1 && n_shards <= 64 && n % n_shards == 0, "yalm_argmax: bad argument");
+	DevBuf dl, dst, dpairs;
+	TRY(up(dl, logits, sizeof(float) * (size_t)n));
+	TRY(up(dst, nullptr, sizeof(StepState)));
+	TRY(up(dpairs, nullptr, sizeof(float) * 2 * n_shards));
+	StepState *st = (StepState *)dst.p;
+	if (n_shards == 1) {
+		argmax_kernel<<<1, 1024>>>((const float *)dl.p, n, st, nullptr, 0);
+	} else { // the tensor-parallel path: per-shard first max as (value, global index), then the pick
+		const int ns = n / n_shards;
+		for (int r = 0; r < n_shards; ++r)
+			argmax_kernel<<<1, 1024>>>((const float *)dl.p + (size_t)r * ns, ns, st, nullptr, 0,
+			                           (float *)dpairs.p + 2 * r, r * ns);
+		argmax_pick_kernel<<<1, 1>>>((const float *)dpairs.p, n_shards, st, nullptr, 0);
+	}
+	HIPCHK(hipGetLastError());
+	HIPCHK(hipDeviceSynchronize());
+	StepState h;
+	HIPCHK(hipMemcpy(&h, st, sizeof(h), hipMemcpyDeviceToHost));
+	*out = h.token;
+	return YALM_OK;
+}
+
 template <class WT>
 static int ffn_t(float *out, const float *x, const void *w1, const void *w2, const void *w3, float *hb, int hidden,
                  int dim, int act) {

@@ -109,6 +109,7 @@ _sig("yalm_decoder_attn_wo", c_int, [c_void_p])
 _sig("yalm_attn_wo_trace", c_int, [c_void_p, c_void_p, ctypes.c_size_t, ctypes.POINTER(c_int), ctypes.POINTER(c_int)])
 _sig("yalm_matmul", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int])
 _sig("yalm_mha", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int])
+_sig("yalm_argmax", c_int, [c_void_p, c_int, c_int, ctypes.POINTER(c_int)])
 _sig("yalm_ffn", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int])
 _sig("yalm_prefill", c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p])
 _sig("yalm_tp_unique_id", c_int, [c_void_p])
@@ -129,6 +130,7 @@ EXPORTED = [
     "yalm_prefill", "yalm_prefill_time", "yalm_gemm_f16", "yalm_attn_prefill", "yalm_tp_unique_id",
     "yalm_decoder_create_tp", "yalm_copy_2d", "yalm_tp_ipc_alloc", "yalm_decoder_create_tp_ipc",
     "yalm_decoder_attn_wo", "yalm_attn_wo_trace", "yalm_stream_envelope",
+    "yalm_argmax",
 ]
 
 HYDRATE_KV_CACHE, OUTPUT_LOGITS = 0, 1
@@ -169,6 +171,15 @@ def mha(kb, vb, q, head_dim, kv_len, max_seq_len, n_heads, n_kv_heads, att_init=
     check(lib.yalm_mha(_ptr(xout), _ptr(att), _ptr(kb), _ptr(vb), _ptr(q), head_dim, kv_len, max_seq_len, n_heads,
                        n_kv_heads))
     return xout, att
+
+
+def argmax(logits: np.ndarray, n_shards: int = 1) -> int:
+    """Device argmax (sampler.cpp:27-38 semantics) of host logits; n_shards > 1:
+    the tensor-parallel per-shard pairs + pick."""
+    lg = np.ascontiguousarray(logits, dtype=np.float32)
+    out = c_int()
+    check(lib.yalm_argmax(_ptr(lg), lg.size, n_shards, ctypes.byref(out)))
+    return out.value
 
 
 def ffn(x, w1, w2, w3, act: int, dtype: int) -> np.ndarray:
@@ -335,17 +346,24 @@ class DeviceModel:
 class Decoder:
     """InferenceState on the device + Model::forward (graph-replayed)."""
 
-    def __init__(self, model: DeviceModel, tp_id: bytes = None, tp_gather=None):
+    def __init__(self, model: DeviceModel, tp_id: bytes = None, tp_gather=None, kv_caches=None):
         """Tensor parallel over model.tp = (rank, size), one of:
         tp_id: the RCCL unique id (tp_unique_id() on rank 0, shared with the
         other ranks); tp_gather: a function mapping this rank's 64-byte IPC
         handle to the list of every rank's handle (e.g. via
         torch.distributed.all_gather_object) for the IPC exchange transport.
-        Neither: a single-GPU decoder."""
+        Neither: a single-GPU decoder. kv_caches: optional per-layer (key, value)
+        device pointers ([max_seq_len][kv_dim] f16 each, caller-owned), as
+        Block::cuda() hands its own caches over (model.cpp:185-211); default: the
+        decoder allocates zeroed caches."""
         self.model = model
         self.cfg = model.cfg
         self._c = Config.from_model(self.cfg)
         mw, self._blocks = model.weights_struct()
+        if kv_caches is not None:
+            for l, (kp, vp) in enumerate(kv_caches):
+                self._blocks[l].key_cache = kp
+                self._blocks[l].value_cache = vp
         self._mw = mw
         h = c_void_p()
         if tp_gather is not None:
