@@ -374,6 +374,37 @@ float orc_sample_prob(const float *logits, int vocab_size, int index) {
 	return expf(logits[index] - max_val) / sum;
 }
 
+/* sampler.cpp:6-9: the Sampler constructor seeds the C library generator */
+void orc_srand(unsigned seed) {
+	srand(seed);
+}
+
+/* sampler.cpp:40-65: temperature sampling by inverse CDF over softmax(logits / T) */
+int orc_sample(const float *logits, int vocab_size, float temperature) {
+	if (temperature == 0.0) {
+		return orc_sample_argmax(logits, vocab_size);
+	}
+	float max_val = -FLT_MAX;
+	for (int i = 0; i < vocab_size; ++i) {
+		if (logits[i] > max_val) {
+			max_val = logits[i];
+		}
+	}
+	float sum = 0;
+	for (int i = 0; i < vocab_size; ++i) {
+		sum += expf((logits[i] - max_val) / temperature);
+	}
+	float r = rand() / (float)RAND_MAX;
+	float cumsum = 0;
+	for (int i = 0; i < vocab_size; ++i) {
+		cumsum += expf((logits[i] - max_val) / temperature) / sum;
+		if (cumsum >= r) {
+			return i;
+		}
+	}
+	return vocab_size - 1;
+}
+
 /* ---- synthetic weights: identical integer hash to yalm_amd/csrc/synth.hip ---- */
 static inline uint64_t splitmix64(uint64_t x) {
 	x += 0x9E3779B97F4A7C15ull;

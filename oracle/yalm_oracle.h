@@ -9,7 +9,8 @@
  *
  * Pinning status: the reference's C++ CPU path cannot
  * be compiled in this image without stand-ins for absent headers
- * (cuda_runtime_api.h, spdlog), so there is no oracle/_ref build. The
+ * (cuda_runtime_api.h, spdlog); oracle/_ref builds only the reference
+ * tokenizer (tokenizer.cpp needs neither). The
  * restatement is pinned by the reference's own known-answer test
  * (test.cpp:68-126, exact), by the reference's CPU-vs-GPU kernel test inputs
  * (test.cpp:148-206, regenerated bit-exactly with libstdc++), and by .yalm
@@ -82,6 +83,8 @@ void orc_forward(const orc_model *m, orc_state *s, int token, int pos, int mode)
 void orc_kv_indices(int max_seq_len, int pos, int *kv_sink, int *kv_pos, int *kv_len);   /* infer.cpp:483-485 */
 int orc_sample_argmax(const float *logits, int vocab_size);                                /* sampler.cpp:27-38 */
 float orc_sample_prob(const float *logits, int vocab_size, int index);                     /* sampler.cpp:11-25 */
+void orc_srand(unsigned seed);                                                             /* sampler.cpp:6-9 */
+int orc_sample(const float *logits, int vocab_size, float temperature);                    /* sampler.cpp:40-65 */
 
 /* Deterministic synthetic weights (same integer hash as the product's device
  * initialiser; used to reproduce the bench's random-weight model on the host). */
