@@ -69,21 +69,48 @@ def spawn_ranks(n):
 
 
 def gpu_state():
-    """Clocks and partition modes as rocm-smi reports them (a separate process;
-    the box's own state explains box-to-box spread)."""
+    """Partition modes and the top DPM level of each clock as rocm-smi reports
+    them (a separate process). The current clock read at idle says nothing about
+    the run, so the envelope measured in-process is the box calibration; this
+    only shows whether a box is partitioned or clock-capped."""
+    import re
+
     out = {}
     try:
-        r = subprocess.run(["rocm-smi", "--showclocks", "--showcomputepartition", "--showmemorypartition", "--json"],
+        r = subprocess.run(["rocm-smi", "--showcomputepartition", "--showmemorypartition", "--json"],
                            capture_output=True, text=True, timeout=30)
         d = json.loads(r.stdout)
         card = d[sorted(d)[0]] if d else {}
-        for k, v in card.items():
-            kl = k.lower()
-            if "sclk" in kl or "mclk" in kl or "fclk" in kl or "partition" in kl:
-                out[k] = v
+        out.update({k: v for k, v in card.items() if "partition" in k.lower()})
+        r = subprocess.run(["rocm-smi", "--showclkfrq"], capture_output=True, text=True, timeout=30)
+        kind = None
+        for line in r.stdout.splitlines():
+            m = re.search(r"Supported (\w+) frequencies", line)
+            if m:
+                kind = m.group(1)
+                continue
+            f = re.search(r"(\d+)\s*Mhz", line, re.I)
+            if kind and f:
+                out[f"{kind}_max_mhz"] = max(out.get(f"{kind}_max_mhz", 0), int(f.group(1)))
     except Exception as e:  # report, never fail the bench on it
         out["error"] = repr(e)[:200]
     return out
+
+
+def cgroup_cpus():
+    """CPUs this process may use by its cgroup CPU quota (v2 cpu.max, v1
+    cfs_quota/period), or None when unlimited / unreadable."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        return None if q == "max" else max(1, int(int(q) / int(p)))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else max(1, q // p)
+    except (OSError, ValueError):
+        return None
 
 
 def cpu_model():
@@ -119,29 +146,23 @@ def pmc_traffic(kernel_match):
 def cpu_baseline(cfg, budget_s):
     """The CPU oracle (oracle/, restatement of the reference -d cpu path with
     its AVX2/F16C GEMV and OpenMP) on the same synthetic weights, timed on
-    this host. Thread count: nproc (BASELINE.md CPU-baseline plan) and the
-    OMP_NUM_THREADS share the harness sets are both probed on a few tokens and
-    the faster one runs the bounded sample (hydrate the prompt, then decode
-    until the budget is spent, at least 2 tokens)."""
+    this host. Threads: nproc (BASELINE.md CPU-baseline plan), capped by the
+    job's cgroup CPU quota -- on the GPU box nproc shows the whole machine (256)
+    while the job may use 16 CPUs, and 256 OpenMP threads there ran 0.03 tok/s
+    (profiles/r3_cpu_threads.txt). Bounded sample: hydrate the prompt, then
+    decode until the budget is spent (at least 2 tokens)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import numpy as np
 
     import oracle_py as O
 
     nproc = len(os.sched_getaffinity(0))
-    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    cands = sorted({c for c in (nproc, share) if c > 0})
+    quota = cgroup_cpus()
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)  # the harness's CPU share when no quota is readable
+    threads = min(nproc, quota or share or nproc)
     host = O.synth_host_tensors_fast(cfg, seed=1)
     om = O.OracleModel(cfg, host)
     prompt = [(7 * i + 1) % cfg.vocab_size for i in range(PROMPT_LEN)]
-    probe = {}
-    for th in cands:  # hydrate the prompt with each candidate (identical work), time it
-        O.set_threads(th)
-        t0 = time.perf_counter()
-        for pos, t in enumerate(prompt[:4]):
-            om.forward(t, pos, 0)
-        probe[th] = 4 / (time.perf_counter() - t0)
-    threads = max(probe, key=probe.get)
     O.set_threads(threads)
     for pos, t in enumerate(prompt):
         om.forward(t, pos, 1 if pos == len(prompt) - 1 else 0)
@@ -163,10 +184,11 @@ def cpu_baseline(cfg, budget_s):
         "kind": "port",
         "cpu_model": cpu_model(),
         "nproc": nproc,
+        "cgroup_cpus": quota,
         "sample": f"oracle -d cpu restatement, {n} greedy decode tokens after a {PROMPT_LEN}-token prompt, "
                   f"same synthetic Mistral-7B {'fp16' if cfg.weight_dtype == 1 else 'fp8'} weights, "
-                  f"{threads} OpenMP threads ({el:.1f} s); thread probe tok/s "
-                  + ", ".join(f"{k}: {v:.2f}" for k, v in sorted(probe.items())),
+                  f"{threads} OpenMP threads = the host CPUs this job may use (nproc {nproc}, "
+                  f"cgroup quota {quota}, OMP_NUM_THREADS {share or 'unset'}), {el:.1f} s",
     }
 
 
