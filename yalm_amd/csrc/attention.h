@@ -17,11 +17,16 @@
 // loads are issued speculatively before kv_len is known (rows past kv_len are
 // read but masked), overlapping the step-state load.
 //  * kv_len <= CHUNK: the workgroup normalises and writes the heads directly.
-//    Longer contexts publish (max, sum, unnormalised out) per chunk with
-//    write-through (sc1) stores and an agent-scope arrival ticket; the last
-//    workgroup of kv head g merges all chunks in chunk order (deterministic)
-//    with sc1 loads — the fence-free hand-off of MI355X_MICROARCH.md
-//    §visibility "Valid forms", row 1.
+//    Longer contexts publish (max, sum, unnormalised out) per chunk as 8-byte
+//    {value, tag} granules (one sc1 store each: the data is its own ready flag,
+//    MI355X_MICROARCH.md §visibility R2); the MERGER -- the highest-index
+//    workgroup with work for kv head g, so every workgroup it waits for was
+//    dispatched before it -- gathers all chunks' granules, re-reading until
+//    every tag holds this launch's tag, and merges them in chunk order
+//    (deterministic). Round 2 used a drained write + agent-scope arrival ticket
+//    + last-arriver merge: three serialised round trips instead of one.
+//    Tags: epoch * n_layers + layer, unique per (forward, layer), so the one
+//    partial buffer serves every layer and is never reset.
 #pragma once
 
 #include <float.h>
@@ -60,21 +65,34 @@ __device__ __forceinline__ void attn_out(float *out, size_t i, float v, unsigned
 	}
 }
 
+#define ATTN_TIMEOUT 200000000ull // 2 s of s_memrealtime (100 MHz): a merger that never sees a chunk gives up
+
+__device__ __forceinline__ unsigned long long gran_ld(const unsigned long long *p) {
+	return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Tag of one attention launch's chunk partials: unique per (forward, layer).
+__device__ __forceinline__ unsigned attn_part_tag(const StepState *step, int layer, int n_layers) {
+	return step->epoch * (unsigned)n_layers + (unsigned)layer;
+}
+
 // One workgroup's share of the split-KV attention: kv head g, key chunks s0,
 // s0 + S, ... `hook()` runs right after the speculative K/V and q loads are
 // issued (attn_wo.h issues its weight stream there, behind them in vmcnt order).
 // Returns true on the workgroup that wrote the final head outputs of kv head g
-// (the single-chunk writer or the last arriver); the result is workgroup-uniform.
+// (the single-chunk writer or the merger); the result is workgroup-uniform.
 // D = head_dim (multiple of 8, D/8 a power of two <= 64); GT >= G.
-// GRAN: outputs as {value, tag} granules into `out` read as unsigned long long[].
+// GRAN: outputs as {value, gtag} granules into `out` read as unsigned long long[].
+// part: [n_heads][nsplit][D + 2] granules tagged ptag (attn_part_tag); err: bit 2
+// set if the merger's bounded wait gave up (results wrong, reported).
 template <int D, int GT, bool GRAN, class Hook>
 // (no __restrict__ here: with it the K/V and q loads may legally sink below the
 // hook's asm barrier once inlined; the standalone kernel keeps it on its arguments)
 __device__ __forceinline__ bool attn_decode_body(bool active, int g, int s0, int S, const float *q, const uint16_t *kc,
                                                  const uint16_t *vc, const StepState *step, int n_heads,
-                                                 int n_kv_heads, int max_seq_len, int nsplit, float *part,
-                                                 unsigned *counters, float *out, float *att_dbg, Hook &&hook,
-                                                 unsigned gtag = 0) {
+                                                 int n_kv_heads, int max_seq_len, int nsplit, unsigned long long *part,
+                                                 unsigned ptag, unsigned *err, float *out, float *att_dbg,
+                                                 Hook &&hook, unsigned gtag = 0) {
 	constexpr int CHUNK = attn_chunk<D>();
 	constexpr int LPK = D / 8;                     // lanes per K/V row, 16 B each
 	constexpr int KPW = 64 / LPK;                  // rows per wave-instruction
@@ -84,7 +102,6 @@ __device__ __forceinline__ bool attn_decode_body(bool active, int g, int s0, int
 	__shared__ float sc[GT][CHUNK];
 	__shared__ __attribute__((aligned(16))) float red[ATTN_WAVES * KPW][GT][D]; // per-row-slot P.V partials
 	__shared__ float ml[GT][2];
-	__shared__ int last_flag;
 
 	const int G = n_heads / n_kv_heads;
 	const int kv_dim = n_kv_heads * D;
@@ -243,60 +260,77 @@ __device__ __forceinline__ bool attn_decode_body(bool active, int g, int s0, int
 			return true;
 		}
 
-		// ---- publish this chunk's partial (o[D], m, l per head) write-through
+		// ---- publish this chunk's partial (o[D], m, l per head) as tagged granules
+		if (att_dbg) // test hook: the raw scores must be visible before the merger sees the tags
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 		for (int i = tid; i < G * D; i += ATTN_THREADS) {
 			const int h = i / D, d = i % D;
 			float o = 0.0f;
 #pragma unroll
 			for (int w = 0; w < ATTN_WAVES * KPW; ++w)
 				o += red[w][h][d];
-			st_sc1(part + ((size_t)(g * G + h) * nsplit + cidx) * (D + 2) + d, o);
+			attn_out<true>((float *)part, ((size_t)(g * G + h) * nsplit + cidx) * (D + 2) + d, o, ptag);
 		}
 		if (tid < G) {
-			float *pp = part + ((size_t)(g * G + tid) * nsplit + cidx) * (D + 2);
-			st_sc1(pp + D, ml[tid][0]);
-			st_sc1(pp + D + 1, ml[tid][1]);
+			const size_t pp = ((size_t)(g * G + tid) * nsplit + cidx) * (D + 2);
+			attn_out<true>((float *)part, pp + D, ml[tid][0], ptag);
+			attn_out<true>((float *)part, pp + D + 1, ml[tid][1], ptag);
 		}
 		__syncthreads(); // LDS (sp, sc, ml, red) reused by the next chunk
 	}
-	asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // every storing wave drains
-	__syncthreads();
-	if (tid == 0) {
-		const int arrivals = min(ns, S); // workgroups with at least one chunk
-		const unsigned ticket = __hip_atomic_fetch_add(&counters[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-		const int last = ticket == (unsigned)(arrivals - 1);
-		if (last) // reset for the next launch (the kernel boundary orders it)
-			__hip_atomic_store(&counters[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-		last_flag = last;
-	}
-	__syncthreads();
-	if (!last_flag)
-		return false;
+	if (s0 != min(ns, S) - 1)
+		return false; // not the merger: nothing to wait for
 
-	// ---- last arriver: merge the ns chunk partials of heads g*G .. in chunk order.
-	// Batches of MB chunks: every (m, l, o[d]) load of a batch is issued before any
-	// is used (one L2 round trip per batch instead of one per chunk), merged with
-	// the online rescaling of flash-decoding; one batch covers kv_len <= 1024.
-	constexpr int MB = 16;
+	// ---- merger: gather the ns chunk partials of heads g*G .. as granules, re-reading
+	// a batch of MB chunks until every tag holds ptag (one round trip when the other
+	// workgroups are done, which they usually are: they started together), then merge
+	// in chunk order with the online rescaling of flash-decoding.
+	constexpr int MB = 8;
 	constexpr int DPL = D >= 64 ? D / 64 : 1; // dims per lane
+	const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + ATTN_TIMEOUT;
+	bool alive = true;
 	for (int h = wave; h < G; h += ATTN_WAVES) {
-		const float *ph = part + (size_t)(g * G + h) * nsplit * (D + 2);
+		const unsigned long long *ph = part + (size_t)(g * G + h) * nsplit * (D + 2);
 		float M = -FLT_MAX, L = 0.0f, o[DPL];
 #pragma unroll
 		for (int k = 0; k < DPL; ++k)
 			o[k] = 0.0f;
-		const bool dl = lane < D; // lanes past D (D < 64) only follow along
+		const int dl = lane < D ? lane : 0; // lanes past D (D < 64) re-read dim 0 and only follow along
 		for (int c0 = 0; c0 < ns; c0 += MB) {
 			float mb[MB], lb[MB], ob[MB][DPL];
+			for (;;) {
+				unsigned long long gm[MB], gl[MB], go[MB][DPL];
 #pragma unroll
-			for (int j = 0; j < MB; ++j) {
-				const int c = min(c0 + j, ns - 1);
-				const float *pc = ph + c * (D + 2);
-				mb[j] = ld_sc1(pc + D);
-				lb[j] = ld_sc1(pc + D + 1);
+				for (int j = 0; j < MB; ++j) {
+					const int c = min(c0 + j, ns - 1);
+					const unsigned long long *pc = ph + (size_t)c * (D + 2);
+					gm[j] = gran_ld(pc + D);
+					gl[j] = gran_ld(pc + D + 1);
 #pragma unroll
-				for (int k = 0; k < DPL; ++k)
-					ob[j][k] = dl ? ld_sc1(pc + lane + 64 * k) : 0.0f;
+					for (int k = 0; k < DPL; ++k)
+						go[j][k] = gran_ld(pc + dl + 64 * k);
+				}
+				bool ok = true;
+#pragma unroll
+				for (int j = 0; j < MB; ++j) {
+					ok = ok && (unsigned)(gm[j] >> 32) == ptag && (unsigned)(gl[j] >> 32) == ptag;
+#pragma unroll
+					for (int k = 0; k < DPL; ++k)
+						ok = ok && (unsigned)(go[j][k] >> 32) == ptag;
+					mb[j] = __uint_as_float((unsigned)gm[j]);
+					lb[j] = __uint_as_float((unsigned)gl[j]);
+#pragma unroll
+					for (int k = 0; k < DPL; ++k)
+						ob[j][k] = __uint_as_float((unsigned)go[j][k]);
+				}
+				if (__all(ok) || !alive)
+					break;
+				__builtin_amdgcn_s_sleep(1);
+				if (__builtin_amdgcn_s_memrealtime() > deadline) {
+					alive = false; // one more pass, then give up (results wrong, reported)
+					if (err && lane == 0)
+						__hip_atomic_fetch_or(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+				}
 			}
 			float Mn = M;
 #pragma unroll
@@ -320,7 +354,7 @@ __device__ __forceinline__ bool attn_decode_body(bool active, int g, int s0, int
 			}
 			M = Mn;
 		}
-		if (dl) {
+		if (lane < D) {
 #pragma unroll
 			for (int k = 0; k < DPL; ++k)
 				attn_out<GRAN>(out, (size_t)(g * G + h) * D + lane + 64 * k, o[k] / L, gtag);
@@ -335,11 +369,15 @@ __device__ __forceinline__ bool attn_decode_body(bool active, int g, int s0, int
 	return true;
 }
 
+// grid (n_kv_heads, S): workgroup (g, s) is dispatched after (g', s') for every
+// s' < s, so the merger (the highest s with work) only waits on earlier ones.
 template <int D, int GT>
 __global__ __launch_bounds__(ATTN_THREADS) void attn_decode_kernel(
     const float *__restrict__ q, const uint16_t *__restrict__ kc, const uint16_t *__restrict__ vc,
     const StepState *__restrict__ step, int n_heads, int n_kv_heads, int max_seq_len, int nsplit,
-    float *__restrict__ part, unsigned *__restrict__ counters, float *__restrict__ out, float *__restrict__ att_dbg) {
-	attn_decode_body<D, GT, false>(true, blockIdx.x, blockIdx.y, gridDim.y, q, kc, vc, step, n_heads, n_kv_heads, max_seq_len,
-	                               nsplit, part, counters, out, att_dbg, [] {});
+    unsigned long long *__restrict__ part, int layer, int n_layers, unsigned *__restrict__ err,
+    float *__restrict__ out, float *__restrict__ att_dbg) {
+	attn_decode_body<D, GT, false>(true, blockIdx.x, blockIdx.y, gridDim.y, q, kc, vc, step, n_heads, n_kv_heads,
+	                               max_seq_len, nsplit, part, attn_part_tag(step, layer, n_layers), err, out, att_dbg,
+	                               [] {});
 }

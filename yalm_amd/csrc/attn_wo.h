@@ -46,8 +46,8 @@
 struct AttnWoArgs {
 	int n_heads, n_kv, max_seq_len, nsplit, S; // S = key-chunk splits per kv head: n_kv * S attention workgroups
 	int q_dim, dim;
-	float *part;        // attention chunk partials (n_heads, nsplit, D + 2)
-	unsigned *counters; // per-kv-head arrival tickets (attention.h)
+	unsigned long long *part; // attention chunk partials (n_heads, nsplit, D + 2) as tagged granules
+	int layer, n_layers;      // partial tag = epoch * n_layers + layer (attention.h)
 	const unsigned long long *gran; // this layer's attention output (q_dim) as {value, epoch} granules
 	const char *wo;     // Wo (dim, q_dim)
 	float *x;           // residual stream (dim)
@@ -206,9 +206,9 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 
 	const unsigned epoch = step->epoch; // this launch's tag (step_begin_kernel / set_step_full_kernel)
 	if (b < units) { // ---- attention workgroup
-		const bool wrote = attn_decode_body<D, GT, true>(true, b % p.n_kv, b / p.n_kv, p.S, q, kc, vc, step,
-		                                                 p.n_heads, p.n_kv, p.max_seq_len, p.nsplit, p.part,
-		                                                 p.counters, (float *)p.gran, nullptr, [] {}, epoch);
+		const bool wrote = attn_decode_body<D, GT, true>(
+		    true, b % p.n_kv, b / p.n_kv, p.S, q, kc, vc, step, p.n_heads, p.n_kv, p.max_seq_len, p.nsplit, p.part,
+		    epoch * (unsigned)p.n_layers + (unsigned)p.layer, p.err, (float *)p.gran, nullptr, [] {}, epoch);
 		if (wrote && tr) // the head outputs are their own ready flags: nothing to drain or signal
 			tr[1] = __builtin_amdgcn_s_memrealtime();
 		if (tr)

@@ -74,8 +74,8 @@ struct yalm_decoder_s {
 	hipStream_t stream = nullptr;
 	bool own_stream = false;
 	StepState *step = nullptr;
-	float *x = nullptr, *q = nullptr, *xb2 = nullptr, *hb = nullptr, *part = nullptr, *logits = nullptr,
-	      *inv_freq = nullptr;
+	float *x = nullptr, *q = nullptr, *xb2 = nullptr, *hb = nullptr, *logits = nullptr, *inv_freq = nullptr;
+	unsigned long long *part = nullptr; // attention chunk partials as {value, tag} granules (attention.h)
 	int *tokens = nullptr;
 	int tokens_cap = 0;
 	float *logits_pinned = nullptr;
@@ -83,7 +83,6 @@ struct yalm_decoder_s {
 	hipGraph_t graph[N_GRAPHS] = {};
 	hipGraphExec_t exec[N_GRAPHS] = {};
 	long long host_pos = -1;         // position of the next forward as the host knows it (-1: unknown)
-	unsigned *attn_counters = nullptr; // per-kv-head arrival tickets (zeroed; the last arriver resets)
 	GemvCfg gemv[GK_N];
 	bool eager = false;     // YALM_EAGER=1: launch kernels directly (profilers that mis-handle graph replay)
 	bool graph_sync = false; // YALM_GRAPH_SYNC=1: synchronise after every replay
@@ -117,7 +116,7 @@ struct yalm_decoder_s {
 	int awo_delay = 0;               // ticks the Wo workgroups wait before their slice loads (YALM_ATTN_WO_DELAY)
 	int awo_spec = 0;                // YALM_AWO_SPEC=1: speculative gather after the slice landed (attn_wo.h)
 	unsigned long long *awo_gran = nullptr; // [n_layers][q_dim] attention outputs as {value, epoch} granules
-	unsigned *awo_err = nullptr;     // error word (bounded spins that gave up)
+	unsigned *awo_err = nullptr;     // error word of the in-launch waits (bit 0 fused Wo gather, bit 1 attention merger)
 };
 
 // ------------------------------------------------------------------ shared helpers

@@ -226,8 +226,8 @@ static bool attn_supported(int head_dim, int G) {
 
 template <int D>
 static void launch_attn_D(int G, const float *q, const uint16_t *kc, const uint16_t *vc, const StepState *step,
-                          int n_heads, int n_kv, int max_seq_len, int nsplit, float *part, unsigned *counters,
-                          float *att, float *out, hipStream_t st) {
+                          int n_heads, int n_kv, int max_seq_len, int nsplit, unsigned long long *part, int layer,
+                          int n_layers, unsigned *err, float *att, float *out, hipStream_t st) {
 	// S key-chunk splits per kv head, each workgroup looping over chunks s, s + S, ...: a grid
 	// sized for max_seq_len would issue the speculative first-chunk loads of every idle
 	// workgroup (15.6 MB of dead KV reads per layer at max_seq_len 4096, kv_len ~150).
@@ -236,7 +236,7 @@ static void launch_attn_D(int G, const float *q, const uint16_t *kc, const uint1
 	dim3 grid(n_kv, std::min(nchunks, splits));
 #define YALM_ATTN(GT)                                                                                                  \
 	attn_decode_kernel<D, GT><<<grid, ATTN_THREADS, 0, st>>>(q, kc, vc, step, n_heads, n_kv, max_seq_len, nsplit,    \
-	                                                         part, counters, out, att)
+	                                                         part, layer, n_layers, err, out, att)
 	if (G <= 1)
 		YALM_ATTN(1);
 	else if (G <= 2)
@@ -253,27 +253,34 @@ static int attn_nsplit(int max_seq_len) {
 	return (max_seq_len + attn_chunk<128>() - 1) / attn_chunk<128>();
 }
 
-// part: (n_heads, nsplit, head_dim + 2) floats; counters: n_kv zeroed words.
+// part: (n_heads, nsplit, head_dim + 2) granules (zeroed once; tags never repeat);
+// err: error word (bit 2: a merger gave up waiting).
 static int launch_attn(int head_dim, int n_heads, int n_kv, const float *q, const uint16_t *kc, const uint16_t *vc,
-                       const StepState *step, int max_seq_len, float *part, unsigned *counters, float *att,
+                       const StepState *step, int max_seq_len, unsigned long long *part, int layer, int n_layers,
+                       unsigned *err, float *att,
                        float *out, hipStream_t st) {
 	const int G = n_heads / n_kv;
 	const int nsplit = attn_nsplit(max_seq_len);
 	switch (head_dim) {
 	case 16:
-		launch_attn_D<16>(G, q, kc, vc, step, n_heads, n_kv, max_seq_len, nsplit, part, counters, att, out, st);
+		launch_attn_D<16>(G, q, kc, vc, step, n_heads, n_kv, max_seq_len, nsplit, part, layer, n_layers, err, att,
+		                   out, st);
 		break;
 	case 32:
-		launch_attn_D<32>(G, q, kc, vc, step, n_heads, n_kv, max_seq_len, nsplit, part, counters, att, out, st);
+		launch_attn_D<32>(G, q, kc, vc, step, n_heads, n_kv, max_seq_len, nsplit, part, layer, n_layers, err, att,
+		                   out, st);
 		break;
 	case 64:
-		launch_attn_D<64>(G, q, kc, vc, step, n_heads, n_kv, max_seq_len, nsplit, part, counters, att, out, st);
+		launch_attn_D<64>(G, q, kc, vc, step, n_heads, n_kv, max_seq_len, nsplit, part, layer, n_layers, err, att,
+		                   out, st);
 		break;
 	case 128:
-		launch_attn_D<128>(G, q, kc, vc, step, n_heads, n_kv, max_seq_len, nsplit, part, counters, att, out, st);
+		launch_attn_D<128>(G, q, kc, vc, step, n_heads, n_kv, max_seq_len, nsplit, part, layer, n_layers, err, att,
+		                   out, st);
 		break;
 	case 256:
-		launch_attn_D<256>(G, q, kc, vc, step, n_heads, n_kv, max_seq_len, nsplit, part, counters, att, out, st);
+		launch_attn_D<256>(G, q, kc, vc, step, n_heads, n_kv, max_seq_len, nsplit, part, layer, n_layers, err, att,
+		                   out, st);
 		break;
 	default:
 		set_err("unsupported head_dim");
@@ -324,7 +331,6 @@ static int attn_wo_init(yalm_decoder_s *d) {
 	// the epoch is >= 1 from the first forward / yalm_block on), then the error word
 	const size_t gran = (size_t)c.n_layers * c.n_heads * c.head_dim;
 	TRY(dalloc(d, (void **)&d->awo_gran, sizeof(unsigned long long) * gran));
-	TRY(dalloc(d, (void **)&d->awo_err, sizeof(unsigned) * AWO_REPL_STRIDE));
 	// key-chunk splits per kv head, as the standalone attention launch (YALM_AWO_SPLITS: sweep knob)
 	const char *senv = getenv("YALM_AWO_SPLITS");
 	d->awo_S = std::min(nchunks, senv ? std::max(1, atoi(senv)) : 32);
@@ -407,7 +413,8 @@ static int launch_attn_wo(yalm_decoder_s *d, const yalm_block_weights &w, int la
 	p.q_dim = c.n_heads * c.head_dim;
 	p.dim = c.dim;
 	p.part = d->part;
-	p.counters = d->attn_counters;
+	p.layer = layer;
+	p.n_layers = c.n_layers;
 	p.gran = d->awo_gran + (size_t)layer * p.q_dim;
 	p.wo = (const char *)w.wo;
 	p.x = d->x;
@@ -536,7 +543,7 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 	} else {
 		if (!(ab & 2))
 			TRY(launch_attn(c.head_dim, c.n_heads, c.n_kv_heads, d->q, w.key_cache, w.value_cache, d->step,
-			                c.max_seq_len, d->part, d->attn_counters, nullptr, d->xb2, st));
+			                c.max_seq_len, d->part, l, c.n_layers, d->awo_err, nullptr, d->xb2, st));
 		if (!(ab & 4))
 			TRY(enqueue_residual_gemv<WT>(d, w.wo, q_dim, d->xb2, GK_WO));
 	}
@@ -790,8 +797,8 @@ static int create_decoder(const yalm_config *config, const yalm_model_weights *w
 	    (r = dalloc(d, (void **)&d->q, sizeof(float) * q_dim)) ||
 	    (r = dalloc(d, (void **)&d->xb2, sizeof(float) * q_dim)) ||
 	    (r = dalloc(d, (void **)&d->hb, sizeof(float) * c.hidden_dim)) ||
-	    (r = dalloc(d, (void **)&d->part, sizeof(float) * (size_t)c.n_heads * nsplit * (c.head_dim + 2))) ||
-	    (r = dalloc(d, (void **)&d->attn_counters, sizeof(unsigned) * c.n_kv_heads)) ||
+	    (r = dalloc(d, (void **)&d->part, sizeof(unsigned long long) * (size_t)c.n_heads * nsplit * (c.head_dim + 2))) ||
+	    (r = dalloc(d, (void **)&d->awo_err, sizeof(unsigned) * AWO_REPL_STRIDE)) ||
 	    (r = dalloc(d, (void **)&d->logits, sizeof(float) * vocab_full)) ||
 	    (r = dalloc(d, (void **)&d->xs, sizeof(float) * c.dim)) ||
 	    (r = dalloc(d, (void **)&d->amax, sizeof(float) * 2)) ||
@@ -1111,7 +1118,7 @@ static int enqueue_one_t(yalm_decoder_s *d, int kernel_id, int l) {
 	}
 	case 1:
 		return launch_attn(c.head_dim, c.n_heads, c.n_kv_heads, d->q, w.key_cache, w.value_cache, d->step,
-		                   c.max_seq_len, d->part, d->attn_counters, nullptr, d->xb2, d->stream);
+		                   c.max_seq_len, d->part, l, c.n_layers, d->awo_err, nullptr, d->xb2, d->stream);
 	case 5:
 		return enqueue_logits_t<WT>(d);
 	case 6:
@@ -1176,7 +1183,7 @@ extern "C" int yalm_time_kernel(yalm_decoder d, int kernel_id, int iters, float 
 	       "bad argument (kernel ids 0-6, 8)");
 	ARGCHK(kernel_id != 6 || d->comm || d->ipc, "kernel 6 (tensor-parallel exchange) needs a tensor-parallel decoder");
 	ARGCHK(kernel_id != 8 || d->attn_wo, "kernel 8 (fused attention + Wo) needs yalm_decoder_attn_wo");
-	const bool bump = kernel_id == 8;
+	const bool bump = kernel_id == 1 || kernel_id == 8; // in-launch hand-offs: fresh tags per launch
 	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_one_t, d, kernel_id, 0)); // warm-up
 	float ms = 0.f;
 	TRY(time_loop(d, kernel_id, iters, bump, true, &ms));
@@ -1382,23 +1389,29 @@ extern "C" int yalm_mha(float *xout, float *att, const uint16_t *kb, const uint1
 	}
 	const size_t kvn = (size_t)max_seq_len * n_kv_heads * head_dim;
 	const int nsplit = attn_nsplit(max_seq_len);
-	DevBuf dk, dv, dq, dout, datt, dpart, dstep, dcnt;
+	DevBuf dk, dv, dq, dout, datt, dpart, dstep, derr;
 	TRY(up(dk, kb, kvn * 2));
 	TRY(up(dv, vb, kvn * 2));
 	TRY(up(dq, q, sizeof(float) * n_heads * head_dim));
 	TRY(up(dout, nullptr, sizeof(float) * n_heads * head_dim));
 	TRY(up(datt, att, sizeof(float) * (size_t)n_heads * max_seq_len));
-	TRY(up(dpart, nullptr, sizeof(float) * (size_t)n_heads * nsplit * (head_dim + 2)));
+	TRY(up(dpart, nullptr, sizeof(unsigned long long) * (size_t)n_heads * nsplit * (head_dim + 2)));
 	TRY(up(dstep, nullptr, sizeof(StepState)));
-	TRY(up(dcnt, nullptr, sizeof(unsigned) * n_kv_heads));
+	TRY(up(derr, nullptr, sizeof(unsigned)));
 	set_step_full_kernel<<<1, 1>>>((StepState *)dstep.p, kv_len - 1, 0, kv_len - 1, kv_len);
 	TRY(launch_attn(head_dim, n_heads, n_kv_heads, (const float *)dq.p, (const uint16_t *)dk.p,
-	                (const uint16_t *)dv.p, (const StepState *)dstep.p, max_seq_len, (float *)dpart.p,
-	                (unsigned *)dcnt.p, att ? (float *)datt.p : nullptr, (float *)dout.p, nullptr));
+	                (const uint16_t *)dv.p, (const StepState *)dstep.p, max_seq_len, (unsigned long long *)dpart.p, 0, 1,
+	                (unsigned *)derr.p, att ? (float *)datt.p : nullptr, (float *)dout.p, nullptr));
 	HIPCHK(hipDeviceSynchronize());
 	HIPCHK(hipMemcpy(xout, dout.p, sizeof(float) * n_heads * head_dim, hipMemcpyDeviceToHost));
 	if (att)
 		HIPCHK(hipMemcpy(att, datt.p, sizeof(float) * (size_t)n_heads * max_seq_len, hipMemcpyDeviceToHost));
+	unsigned e = 0;
+	HIPCHK(hipMemcpy(&e, derr.p, sizeof(e), hipMemcpyDeviceToHost));
+	if (e) {
+		set_err("yalm_mha: the split-KV merger gave up waiting for a chunk");
+		return YALM_ERR_HIP;
+	}
 	return YALM_OK;
 }
 
