@@ -44,12 +44,12 @@ def relerr(a, b):
     return float(np.max(np.abs(a - b)) / (np.max(np.abs(b)) + 1e-30))
 
 
-# hand-off variants: "default"; "spec" = speculative granule gather once the Wo
-# slice has landed (YALM_AWO_SPEC=1, its fallback = sentinel poll + re-gather
-# when a tag is stale); "lag" = no Wo start delay and the spec path (the
-# attention lags the slice, so the miss path runs); "nodelay" = no start delay
-VARIANTS = {"default": {}, "spec": {"YALM_AWO_SPEC": "1"},
-            "lag": {"YALM_AWO_SPEC": "1", "YALM_ATTN_WO_DELAY": "0"}, "nodelay": {"YALM_ATTN_WO_DELAY": "0"}}
+# hand-off variants (attn_wo.h awo_gather_gran): "default" = gather + sentinels in
+# one round trip once the Wo slice has landed, falling back to the sentinel poll +
+# re-gather when a tag is stale; "nospec" = poll first (YALM_AWO_SPEC=0); "lag" =
+# no Wo start delay, so at long contexts the attention lags the slice and the
+# fallback path runs
+VARIANTS = {"default": {}, "nospec": {"YALM_AWO_SPEC": "0"}, "lag": {"YALM_ATTN_WO_DELAY": "0"}}
 
 
 def make(cfg, seed, fused=True, t=None, variant="default", extra=None):
@@ -78,7 +78,7 @@ def make(cfg, seed, fused=True, t=None, variant="default", extra=None):
     return t, dm, dec
 
 
-@pytest.mark.parametrize("variant", ["default", "spec"])
+@pytest.mark.parametrize("variant", ["default", "nospec"])
 @pytest.mark.parametrize("name,cfg", CASES, ids=[c[0] for c in CASES])
 def test_attn_wo_forward_and_greedy_vs_oracle(name, cfg, variant):
     """OUTPUT-mode logits at every position (hydrated prompt first), through
@@ -108,7 +108,7 @@ def test_attn_wo_forward_and_greedy_vs_oracle(name, cfg, variant):
         dm.close()
 
 
-@pytest.mark.parametrize("variant", ["default", "spec", "lag"])
+@pytest.mark.parametrize("variant", ["default", "nospec", "lag"])
 @pytest.mark.parametrize("name,cfg", CASES[:2] + CASES[4:5], ids=[c[0] for c in CASES[:2] + CASES[4:5]])
 def test_attn_wo_matches_separate_launches(name, cfg, variant):
     """Same weights, same tokens: fused vs separate attention and Wo launches

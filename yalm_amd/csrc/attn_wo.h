@@ -85,12 +85,40 @@ __device__ __forceinline__ void awo_ld8_sc1(u32x4_t (&v)[8], const void *const (
 	             : "memory");
 }
 
+// The same eight loads plus one 8-byte sc1 load of a sentinel granule, one vmcnt(0).
+__device__ __forceinline__ void awo_ld8s_sc1(u32x4_t (&v)[8], const void *const (&a)[8], unsigned long long &sv,
+                                             const void *sp) {
+	asm volatile("global_load_dwordx4 %0, %9, off sc1\n\t"
+	             "global_load_dwordx4 %1, %10, off sc1\n\t"
+	             "global_load_dwordx4 %2, %11, off sc1\n\t"
+	             "global_load_dwordx4 %3, %12, off sc1\n\t"
+	             "global_load_dwordx4 %4, %13, off sc1\n\t"
+	             "global_load_dwordx4 %5, %14, off sc1\n\t"
+	             "global_load_dwordx4 %6, %15, off sc1\n\t"
+	             "global_load_dwordx4 %7, %16, off sc1\n\t"
+	             "global_load_dwordx2 %8, %17, off sc1\n\t"
+	             "s_waitcnt vmcnt(0)"
+	             : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]),
+	               "=&v"(v[7]), "=&v"(sv)
+	             : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "v"(sp)
+	             : "memory");
+}
+
 // This lane's XS pieces of the attention output (EPL columns each, pieces
-// ATTN_THREADS * EPL columns apart) as {value, tag} granules: first one sentinel
-// granule per covered head is polled, then 16-byte sc1 loads (two granules each)
-// in batches of 8, each batch re-read until all its tags equal `tag` across the
-// wave (the check that makes it correct). False if the bounded spin gave up
-// (deadline, s_memrealtime).
+// ATTN_THREADS * EPL columns apart) as {value, tag} granules, gathered with
+// 16-byte sc1 loads (two granules each) in batches of 8, each batch re-read until
+// all its tags equal `tag` across the wave (the check that makes it correct).
+// Nothing is issued before this wave's Wo slice has landed: a load samples memory
+// when the memory system executes it, so one issued at launch start (behind the
+// slice in the CU's queue, its result usable only once the slice is in, vmcnt
+// being in order) would return a stale sample and cost a second round trip.
+// First attempt: batch 0 together with one sentinel granule per covered head (the
+// head's last element). All tags fresh: done in ONE round trip (the heads are
+// usually written by the time the slice lands). Otherwise, if the sentinels are
+// fresh, only the re-gather is left; if not, the cheap sentinel poll (one 8-byte
+// load per lane) runs before the full re-reads. `spec` = 0 (YALM_AWO_SPEC=0)
+// skips the combined first attempt. False if the bounded spin gave up (deadline,
+// s_memrealtime).
 template <int EPL, int XS>
 __device__ __forceinline__ bool awo_gather_gran(float (&xs)[XS][EPL], const unsigned long long *gran, int tid,
                                                 unsigned tag, unsigned long long deadline, bool spec) {
@@ -100,46 +128,59 @@ __device__ __forceinline__ bool awo_gather_gran(float (&xs)[XS][EPL], const unsi
 	constexpr int D = 128;
 	constexpr int HPP = 64 * EPL / D; // heads per piece (4 or 8)
 	bool alive = true;
-	// speculative gather (spec, single-batch shapes): issued only once this wave's Wo slice
-	// has landed (a load samples memory when it is ISSUED; issued earlier it would read
-	// stale tags), by which time the heads are usually written: when every tag matches,
-	// the sentinel poll and its extra round trip are skipped; otherwise fall through
-	if (spec && NB == 1) {
-		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-		const void *a[8];
+	const int lane = tid & 63, wave = tid >> 6;
+	const unsigned long long *sent;
+	{
+		const int l = lane < XS * HPP ? lane : 0;
+		const int k = l / HPP;
+		const int h = (k * ATTN_THREADS + 64 * wave) * EPL / D + l % HPP;
+		sent = gran + (size_t)h * D + (D - 1);
+	}
+	auto addrs = [&](int bt, const void *(&a)[8]) {
 #pragma unroll
 		for (int i = 0; i < 8; ++i) {
-			const int l = i < NL ? i : 0;
+			const int l = bt * 8 + (i < NL - bt * 8 ? i : 0); // pad a short batch with a repeat
 			const int k = l / LPP, e = (l % LPP) * 2;
 			a[i] = gran + (size_t)(k * ATTN_THREADS + tid) * EPL + e;
 		}
-		u32x4_t v[8];
-		awo_ld8_sc1(v, a);
+	};
+	auto take = [&](int bt, const u32x4_t (&v)[8]) {
+#pragma unroll
+		for (int i = 0; i < 8; ++i) {
+			if (i < NL - bt * 8) {
+				const int l = bt * 8 + i;
+				const int k = l / LPP, e = (l % LPP) * 2;
+				const uint32_t w0 = v[i][0], w1 = v[i][2];
+				xs[k][e] = __uint_as_float(w0);
+				xs[k][e + 1] = __uint_as_float(w1);
+			}
+		}
+	};
+	auto fresh = [&](const u32x4_t (&v)[8]) {
 		bool ok = true;
 #pragma unroll
 		for (int i = 0; i < 8; ++i)
 			ok = ok && v[i][1] == tag && v[i][3] == tag;
-		if (__all(ok)) {
-#pragma unroll
-			for (int i = 0; i < 8; ++i) {
-				if (i < NL) {
-					const int k = i / LPP, e = (i % LPP) * 2;
-					const uint32_t w0 = v[i][0], w1 = v[i][2];
-					xs[k][e] = __uint_as_float(w0);
-					xs[k][e + 1] = __uint_as_float(w1);
-				}
-			}
-			return true;
+		return __all(ok);
+	};
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the slice has landed
+	bool sent_ok = false;
+	int bt0 = 0;
+	if (spec) {
+		const void *a[8];
+		addrs(0, a);
+		u32x4_t v[8];
+		unsigned long long sv;
+		awo_ld8s_sc1(v, a, sv, sent);
+		sent_ok = __all((unsigned)(sv >> 32) == tag);
+		if (fresh(v)) {
+			take(0, v);
+			bt0 = 1;
+			if (NB == 1)
+				return true;
 		}
 	}
-	// cheap wait first: one lane per covered head polls that head's last granule
-	// (one 8-byte sc1 load per lane), so the full re-reads below run ~once
-	{
-		const int lane = tid & 63, wave = tid >> 6;
-		const int l = lane < XS * HPP ? lane : 0;
-		const int k = l / HPP;
-		const int h = (k * ATTN_THREADS + 64 * wave) * EPL / D + l % HPP;
-		const unsigned long long *sent = gran + (size_t)h * D + (D - 1);
+	if (!sent_ok) {
 		for (;;) {
 			const unsigned long long g = __hip_atomic_load(sent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 			if (__all((unsigned)(g >> 32) == tag))
@@ -153,38 +194,20 @@ __device__ __forceinline__ bool awo_gather_gran(float (&xs)[XS][EPL], const unsi
 	}
 #pragma unroll
 	for (int bt = 0; bt < NB; ++bt) {
+		if (bt < bt0)
+			continue;
 		const void *a[8];
-#pragma unroll
-		for (int i = 0; i < 8; ++i) {
-			const int l = bt * 8 + (i < NL - bt * 8 ? i : 0); // pad a short batch with a repeat
-			const int k = l / LPP, e = (l % LPP) * 2;
-			a[i] = gran + (size_t)(k * ATTN_THREADS + tid) * EPL + e;
-		}
+		addrs(bt, a);
 		u32x4_t v[8];
 		for (;;) {
 			awo_ld8_sc1(v, a);
-			bool ok = true;
-#pragma unroll
-			for (int i = 0; i < 8; ++i) {
-				const uint32_t t0 = v[i][1], t1 = v[i][3];
-				ok = ok && t0 == tag && t1 == tag;
-			}
-			if (__all(ok) || !alive)
+			if (fresh(v) || !alive)
 				break;
 			__builtin_amdgcn_s_sleep(1);
 			if (__builtin_amdgcn_s_memrealtime() > deadline)
 				alive = false; // one more pass, then give up (results wrong, reported)
 		}
-#pragma unroll
-		for (int i = 0; i < 8; ++i) {
-			if (i < NL - bt * 8) {
-				const int l = bt * 8 + i;
-				const int k = l / LPP, e = (l % LPP) * 2;
-				const uint32_t w0 = v[i][0], w1 = v[i][2];
-				xs[k][e] = __uint_as_float(w0);
-				xs[k][e + 1] = __uint_as_float(w1);
-			}
-		}
+		take(bt, v);
 	}
 	return alive;
 }

@@ -348,11 +348,12 @@ static int attn_wo_init(yalm_decoder_s *d) {
 	// stream (tools/sweep_awo.sh, profiles/r2_sweep_awo_delay.txt: 10.6 -> 10.1 us at kv_len 17,
 	// 10.6 -> 10.4 at kv_len 151; 0.4-0.6 us delays lose it again at long contexts)
 	d->awo_delay = denv ? std::max(0, atoi(denv)) : 20;
-	// speculative gather (opt-in): the round-2 A/B that made it the default timed
-	// back-to-back launches whose granules already held the current epoch, i.e. with no
-	// attention -> Wo dependency; yalm_time_kernel now advances the epoch per launch
+	// combined first attempt (gather + sentinels in one round trip once the slice has
+	// landed, attn_wo.h awo_gather_gran); YALM_AWO_SPEC=0 skips it (A/B knob). Round 2's
+	// speculative gather was chosen from back-to-back launches whose granules already held
+	// the current epoch; yalm_time_kernel now gives each timed launch a fresh one
 	const char *spenv = getenv("YALM_AWO_SPEC");
-	d->awo_spec = spenv ? atoi(spenv) != 0 : 0;
+	d->awo_spec = spenv ? atoi(spenv) != 0 : 1;
 	const char *tenv = getenv("YALM_ATTN_WO_TRACE");
 	if (tenv && atoi(tenv) != 0)
 		TRY(dalloc(d, (void **)&d->awo_trace, sizeof(unsigned long long) * 4 * d->awo_nb));
