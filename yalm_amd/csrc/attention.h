@@ -76,6 +76,19 @@ __device__ __forceinline__ unsigned attn_part_tag(const StepState *step, int lay
 	return step->epoch * (unsigned)n_layers + (unsigned)layer;
 }
 
+// Head outputs of the fused launch: `reps` copies, `stride` granules apart (one per
+// XCD-group of consumers, attn_wo.h AWO_GR), so the 256 consumer workgroups' reads
+// spread over `reps` x the addresses.
+template <bool GRAN>
+__device__ __forceinline__ void attn_out_rep(float *out, size_t i, float v, unsigned tag, int reps, size_t stride) {
+	if constexpr (GRAN) {
+		for (int r = 0; r < reps; ++r)
+			attn_out<true>(out, i + (size_t)r * stride, v, tag);
+	} else {
+		out[i] = v;
+	}
+}
+
 // One workgroup's share of the split-KV attention: kv head g, key chunks s0,
 // s0 + S, ... `hook()` runs right after the speculative K/V and q loads are
 // issued (attn_wo.h issues its weight stream there, behind them in vmcnt order).
@@ -92,7 +105,7 @@ __device__ __forceinline__ bool attn_decode_body(bool active, int g, int s0, int
                                                  const uint16_t *vc, const StepState *step, int n_heads,
                                                  int n_kv_heads, int max_seq_len, int nsplit, unsigned long long *part,
                                                  unsigned ptag, unsigned *err, float *out, float *att_dbg,
-                                                 Hook &&hook, unsigned gtag = 0) {
+                                                 Hook &&hook, unsigned gtag = 0, int greps = 1) {
 	constexpr int CHUNK = attn_chunk<D>();
 	constexpr int LPK = D / 8;                     // lanes per K/V row, 16 B each
 	constexpr int KPW = 64 / LPK;                  // rows per wave-instruction
@@ -249,7 +262,7 @@ __device__ __forceinline__ bool attn_decode_body(bool active, int g, int s0, int
 #pragma unroll
 				for (int w = 0; w < ATTN_WAVES * KPW; ++w)
 					o += red[w][h][d];
-				attn_out<GRAN>(out, (size_t)(g * G + h) * D + d, o / ml[h][1], gtag);
+				attn_out_rep<GRAN>(out, (size_t)(g * G + h) * D + d, o / ml[h][1], gtag, greps, (size_t)n_heads * D);
 			}
 			if (att_dbg) {
 				for (int i = tid; i < G * nt; i += ATTN_THREADS) {
@@ -357,7 +370,8 @@ __device__ __forceinline__ bool attn_decode_body(bool active, int g, int s0, int
 		if (lane < D) {
 #pragma unroll
 			for (int k = 0; k < DPL; ++k)
-				attn_out<GRAN>(out, (size_t)(g * G + h) * D + lane + 64 * k, o[k] / L, gtag);
+				attn_out_rep<GRAN>(out, (size_t)(g * G + h) * D + lane + 64 * k, o[k] / L, gtag, greps,
+				                   (size_t)n_heads * D);
 		}
 		if (att_dbg) {
 			for (int t = lane; t < kv_len; t += 64) {

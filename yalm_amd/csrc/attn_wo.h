@@ -42,6 +42,7 @@
 #define AWO_RPW 16                   // Wo rows per Wo workgroup (256 of them for Mistral-7B)
 #define AWO_TIMEOUT 200000000ull     // 2 s of s_memrealtime (100 MHz)
 #define AWO_REPL_STRIDE 32           // words of the error slot (a 128-B line of its own)
+#define AWO_GR 8                     // max copies of the head outputs per layer (one per XCD)
 
 struct AttnWoArgs {
 	int n_heads, n_kv, max_seq_len, nsplit, S; // S = key-chunk splits per kv head: n_kv * S attention workgroups
@@ -58,6 +59,7 @@ struct AttnWoArgs {
 	int delay;          // s_memrealtime ticks (10 ns) the Wo workgroups wait before their slice loads
 	                    // (YALM_ATTN_WO_DELAY, tuning knob: lets the attention chain start alone)
 	int spec;           // speculative gather once the slice has landed (YALM_AWO_SPEC)
+	int greps;          // copies of the head outputs (YALM_AWO_REPL, <= AWO_GR); Wo workgroup j reads copy j % greps
 };
 
 // Eight 16-byte sc1 loads from arbitrary addresses in one statement, one vmcnt(0)
@@ -231,7 +233,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 	if (b < units) { // ---- attention workgroup
 		const bool wrote = attn_decode_body<D, GT, true>(
 		    true, b % p.n_kv, b / p.n_kv, p.S, q, kc, vc, step, p.n_heads, p.n_kv, p.max_seq_len, p.nsplit, p.part,
-		    epoch * (unsigned)p.n_layers + (unsigned)p.layer, p.err, (float *)p.gran, nullptr, [] {}, epoch);
+		    epoch * (unsigned)p.n_layers + (unsigned)p.layer, p.err, (float *)p.gran, nullptr, [] {}, epoch, p.greps);
 		if (wrote && tr) // the head outputs are their own ready flags: nothing to drain or signal
 			tr[1] = __builtin_amdgcn_s_memrealtime();
 		if (tr)
@@ -277,7 +279,8 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 	// only for the heads its columns cover), then dot them into every resident row.
 	const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 	float xs[XS][EPL];
-	if (!awo_gather_gran<EPL, XS>(xs, p.gran, tid, epoch, t0 + AWO_TIMEOUT, p.spec != 0) && lane == 0)
+	const unsigned long long *gran = p.gran + (size_t)(j % p.greps) * p.q_dim;
+	if (!awo_gather_gran<EPL, XS>(xs, gran, tid, epoch, t0 + AWO_TIMEOUT, p.spec != 0) && lane == 0)
 		__hip_atomic_fetch_or(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 	if (tr)
 		tr[2] = __builtin_amdgcn_s_memrealtime();

@@ -115,7 +115,8 @@ struct yalm_decoder_s {
 	int awo_win = 0;                 // Wo loads in flight per lane (YALM_ATTN_WO_WIN), -1 = none (ablation)
 	int awo_delay = 0;               // ticks the Wo workgroups wait before their slice loads (YALM_ATTN_WO_DELAY)
 	int awo_spec = 0;                // YALM_AWO_SPEC=1: speculative gather after the slice landed (attn_wo.h)
-	unsigned long long *awo_gran = nullptr; // [n_layers][q_dim] attention outputs as {value, epoch} granules
+	unsigned long long *awo_gran = nullptr; // [n_layers][AWO_GR][q_dim] attention outputs as {value, epoch} granules
+	int awo_greps = 1;               // copies written / read (YALM_AWO_REPL)
 	unsigned *awo_err = nullptr;     // error word of the in-launch waits (bit 0 fused Wo gather, bit 1 attention merger)
 };
 

@@ -329,7 +329,7 @@ static int attn_wo_init(yalm_decoder_s *d) {
 	const int nchunks = (c.max_seq_len + attn_chunk<128>() - 1) / attn_chunk<128>();
 	// per layer: the attention output as {value, epoch} granules (zero tags never match:
 	// the epoch is >= 1 from the first forward / yalm_block on), then the error word
-	const size_t gran = (size_t)c.n_layers * c.n_heads * c.head_dim;
+	const size_t gran = (size_t)c.n_layers * AWO_GR * c.n_heads * c.head_dim;
 	TRY(dalloc(d, (void **)&d->awo_gran, sizeof(unsigned long long) * gran));
 	// key-chunk splits per kv head, as the standalone attention launch (YALM_AWO_SPLITS: sweep knob)
 	const char *senv = getenv("YALM_AWO_SPLITS");
@@ -349,11 +349,16 @@ static int attn_wo_init(yalm_decoder_s *d) {
 	// 10.6 -> 10.4 at kv_len 151; 0.4-0.6 us delays lose it again at long contexts)
 	d->awo_delay = denv ? std::max(0, atoi(denv)) : 20;
 	// combined first attempt (gather + sentinels in one round trip once the slice has
-	// landed, attn_wo.h awo_gather_gran); YALM_AWO_SPEC=0 skips it (A/B knob). Round 2's
-	// speculative gather was chosen from back-to-back launches whose granules already held
-	// the current epoch; yalm_time_kernel now gives each timed launch a fresh one
+	// landed, attn_wo.h awo_gather_gran): opt-in, YALM_AWO_SPEC=1. Measured with a fresh
+	// epoch per timed launch it loses (profiles/r3_ab_awo.txt): fp8 kv 17
+	// 9.2 -> 11.0 us, fp16 kv 151 11.2 -> 12.0-12.6; the all-waves gather burst costs more
+	// than the poll round trip it saves
 	const char *spenv = getenv("YALM_AWO_SPEC");
-	d->awo_spec = spenv ? atoi(spenv) != 0 : 1;
+	d->awo_spec = spenv ? atoi(spenv) != 0 : 0;
+	// copies of the head outputs the Wo workgroups read (one per XCD: the 256 consumers'
+	// gathers spread over 8x the addresses); YALM_AWO_REPL in 1..AWO_GR
+	const char *renv = getenv("YALM_AWO_REPL");
+	d->awo_greps = renv ? std::max(1, std::min(AWO_GR, atoi(renv))) : 1;
 	const char *tenv = getenv("YALM_ATTN_WO_TRACE");
 	if (tenv && atoi(tenv) != 0)
 		TRY(dalloc(d, (void **)&d->awo_trace, sizeof(unsigned long long) * 4 * d->awo_nb));
@@ -416,7 +421,8 @@ static int launch_attn_wo(yalm_decoder_s *d, const yalm_block_weights &w, int la
 	p.part = d->part;
 	p.layer = layer;
 	p.n_layers = c.n_layers;
-	p.gran = d->awo_gran + (size_t)layer * p.q_dim;
+	p.gran = d->awo_gran + (size_t)layer * AWO_GR * p.q_dim;
+	p.greps = d->awo_greps;
 	p.wo = (const char *)w.wo;
 	p.x = d->x;
 	p.err = d->awo_err;
