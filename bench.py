@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--tp-transport", default="rccl", choices=["rccl", "ipc"],
                     help="all-reduce transport for tensor parallelism: RCCL (one rank per GPU) or the IPC one-shot exchange")
     ap.add_argument("--no-envelope", action="store_true")
+    ap.add_argument("--no-gpu-state", action="store_true",
+                    help="skip the rocm-smi query (under a profiler: its preload would run inside rocm-smi too)")
     return ap.parse_args()
 
 
@@ -241,7 +243,8 @@ def main():
         dist_mod.init_process_group("gloo")
         dist = dist_mod
 
-    state = gpu_state() if local_rank == 0 else None
+    profiled = any(k.startswith("ROCPROF") for k in os.environ)
+    state = gpu_state() if local_rank == 0 and not (args.no_gpu_state or profiled) else None
     from yalm_amd import models as M
     from yalm_amd import runtime
 
