@@ -41,14 +41,18 @@ def test_gemm_exact_integers(M_, N, K):
 
 # GEMM forms (yalm_amd/csrc/prefill.h gemm_nt_kernel): LDS-DMA stages 2 / 3 and the
 # 128 x 256 ("wide") tile; read per launch from the environment
-FORMS = {"auto": {}, "s2": {"YALM_PF_STAGES": "2"}, "s3": {"YALM_PF_STAGES": "3"},
-         "s3-wide": {"YALM_PF_STAGES": "3", "YALM_PF_WIDE": "1"},
-         "s2-wide": {"YALM_PF_STAGES": "2", "YALM_PF_WIDE": "1"},
-         "s3-narrow": {"YALM_PF_STAGES": "3", "YALM_PF_WIDE": "0"}}
+# (the 128-tile forms switch the large-tile kernel off: YALM_PF_G16=0); "g16-256" /
+# "g16-128": prefill_gemm.h gemm16_kernel with 256 x 256 / 256 x 128 tiles everywhere
+G16_ALL = "qkv:{0},wo:{0},glu:{0},w2:{0},cls:{0},test:{0}"
+FORMS = {"auto": {}, "s2": {"YALM_PF_STAGES": "2", "YALM_PF_G16": "0"}, "s3": {"YALM_PF_STAGES": "3", "YALM_PF_G16": "0"},
+         "s3-wide": {"YALM_PF_STAGES": "3", "YALM_PF_WIDE": "1", "YALM_PF_G16": "0"},
+         "s2-wide": {"YALM_PF_STAGES": "2", "YALM_PF_WIDE": "1", "YALM_PF_G16": "0"},
+         "s3-narrow": {"YALM_PF_STAGES": "3", "YALM_PF_WIDE": "0", "YALM_PF_G16": "0"},
+         "g16-256": {"YALM_PF_G16": G16_ALL.format(256)}, "g16-128": {"YALM_PF_G16": G16_ALL.format(128)}}
 
 
 @pytest.mark.parametrize("form", list(FORMS))
-@pytest.mark.parametrize("M_,N,K", [(200, 256, 192), (37, 768, 128), (1, 256, 64), (513, 5120, 640)])
+@pytest.mark.parametrize("M_,N,K", [(200, 256, 192), (37, 768, 128), (1, 256, 64), (513, 5120, 640), (300, 384, 64)])
 def test_gemm_forms_exact(form, M_, N, K, monkeypatch):
     """Every stage count / tile form is exact on f16-exact integer data (any
     staging race or fragment-map error shows as a wrong integer); K tiles 1..10."""
@@ -118,7 +122,7 @@ CFGS = {
 }
 
 
-@pytest.mark.parametrize("form", ["auto", "s3", "s2-wide"])
+@pytest.mark.parametrize("form", ["auto", "s3", "s2-wide", "g16-256", "g16-128"])
 def test_prefill_forms_match_decode(form, monkeypatch):
     """The whole prefill in each GEMM form (the wide tile on every GEMM with N %
     256 == 0, incl. the vocab-tiled logits epilogue run once per column half)."""

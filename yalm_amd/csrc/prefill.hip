@@ -1,4 +1,5 @@
 #include <cstdlib>
+#include <cstring>
 // prefill.hip — C ABI of the batched prefill / perplexity path (prefill.h):
 // yalm_prefill (prompt hydration + per-position log p(next), replacing the
 // reference's position-by-position loop in main.cpp:128-200 / 102-112) and
@@ -11,6 +12,7 @@
 
 #include "decoder.h"
 #include "prefill.h"
+#include "prefill_gemm.h"
 
 namespace {
 
@@ -59,6 +61,57 @@ int launch_gemm(const uint16_t *A, int M, int K, pf::BSrc b0, pf::BSrc b1, int N
 	void *args[] = {(void *)&A, (void *)&M, (void *)&K, (void *)&b0, (void *)&b1, (void *)&N, (void *)&epi};
 	HIPCHK(hipLaunchKernel(kern, dim3(nwg), dim3(pf::THREADS), args, lds, st));
 	HIPCHK(hipGetLastError());
+	return YALM_OK;
+}
+
+// Large-tile GEMM form per GEMM kind (prefill_gemm.h): 0 = the 128 x 128 kernel,
+// 256 / 128 = gemm16_kernel with a 256 x BN tile. YALM_PF_G16 = "qkv:256,wo:128,..."
+// overrides (read per launch: tests switch it inside one process).
+enum { PG_QKV = 0, PG_WO = 1, PG_GLU = 2, PG_W2 = 3, PG_CLS = 4, PG_TEST = 5 };
+int g16_form(int kind) {
+	static const int defaults[6] = {256, 128, 256, 128, 256, 256};
+	static const char *names[6] = {"qkv", "wo", "glu", "w2", "cls", "test"};
+	int f = defaults[kind];
+	if (const char *e = getenv("YALM_PF_G16")) {
+		if (!strcmp(e, "0"))
+			return 0;
+		const char *p = strstr(e, names[kind]);
+		if (p && p[strlen(names[kind])] == ':')
+			f = atoi(p + strlen(names[kind]) + 1);
+	}
+	return f == 256 || f == 128 ? f : 0;
+}
+
+template <class EPI, class BMAP, int BN, int WM>
+int launch_g16_t(const uint16_t *A, int M, int K, const BMAP &bm, int N, const EPI &epi, hipStream_t st) {
+	auto kern = pf::gemm16_kernel<EPI, BMAP, BN, WM>;
+	constexpr size_t lds = pf::gemm16_lds<BN>();
+	static bool attr = false;
+	if (!attr) {
+		HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+		attr = true;
+	}
+	const int nwg = ((M + pf::G_BM - 1) / pf::G_BM) * (N / BN);
+	hipLaunchKernelGGL(kern, dim3(nwg), dim3(pf::G_THREADS), lds, st, A, M, K, bm, N, epi);
+	HIPCHK(hipGetLastError());
+	return YALM_OK;
+}
+
+// C = A · W^T through the large-tile kernel when the form allows (N % BN == 0),
+// else false (the caller launches gemm_nt_kernel).
+template <class EPI>
+int launch_g16_plain(int form, const uint16_t *A, int M, int K, const pf::BSrc &b, int N, const EPI &epi,
+                     hipStream_t st, bool &done) {
+	done = false;
+	pf::BRowsPlain bm{b};
+	if (form == 256 && N % 256 == 0) {
+		done = true;
+		return launch_g16_t<EPI, pf::BRowsPlain, 256, 2>(A, M, K, bm, N, epi, st);
+	}
+	if (form == 128 && N % 128 == 0) {
+		done = true;
+		return launch_g16_t<EPI, pf::BRowsPlain, 128, 4>(A, M, K, bm, N, epi, st);
+	}
 	return YALM_OK;
 }
 
@@ -134,6 +187,21 @@ int ensure_bufs(yalm_decoder_s *d) {
 template <int ACT>
 int enqueue_glu(yalm_decoder_s *d, const yalm_block_weights &w, int T) {
 	const yalm_config &c = d->c;
+	const int form = g16_form(PG_GLU);
+	if (form && c.hidden_dim % (form / 2) == 0) {
+		pf::E16Glu<ACT> e;
+		e.h = d->pf.H;
+		e.ldh = c.hidden_dim;
+		e.M = T;
+		if (form == 256) {
+			pf::BRowsGlu<64> bm{(const uint16_t *)w.w1, (const uint16_t *)w.w3};
+			return launch_g16_t<pf::E16Glu<ACT>, pf::BRowsGlu<64>, 256, 2>(d->pf.Xn, T, c.dim, bm, 2 * c.hidden_dim,
+			                                                             e, d->stream);
+		}
+		pf::BRowsGlu<64> bm{(const uint16_t *)w.w1, (const uint16_t *)w.w3};
+		return launch_g16_t<pf::E16Glu<ACT>, pf::BRowsGlu<64>, 128, 4>(d->pf.Xn, T, c.dim, bm, 2 * c.hidden_dim, e,
+		                                                             d->stream);
+	}
 	pf::EpiGlu<ACT> e;
 	e.h = d->pf.H;
 	e.ldh = c.hidden_dim;
@@ -165,6 +233,21 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 			qkv.end[0] = q_dim;
 			qkv.end[1] = q_dim + kv_dim;
 			qkv.end[2] = q_dim + 2 * kv_dim;
+			bool done = false;
+			{
+				pf::E16QKV e;
+				e.q = b.Q;
+				e.kc = w.key_cache;
+				e.vc = w.value_cache;
+				e.rope = b.rope;
+				e.M = T;
+				e.q_dim = q_dim;
+				e.kv_dim = kv_dim;
+				e.head_dim = c.head_dim;
+				e.pos0 = pos0;
+				e.clip = c.qkv_clip;
+				TRY(launch_g16_plain(g16_form(PG_QKV), b.Xn, T, c.dim, qkv, q_dim + 2 * kv_dim, e, st, done));
+			}
 			pf::EpiQKV e;
 			e.q = b.Q;
 			e.kc = w.key_cache;
@@ -176,7 +259,8 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 			e.head_dim = c.head_dim;
 			e.pos0 = pos0;
 			e.clip = c.qkv_clip;
-			TRY((launch_gemm<pf::EpiQKV, 1>(b.Xn, T, c.dim, qkv, qkv, q_dim + 2 * kv_dim, e, st)));
+			if (!done)
+				TRY((launch_gemm<pf::EpiQKV, 1>(b.Xn, T, c.dim, qkv, qkv, q_dim + 2 * kv_dim, e, st)));
 		}
 		TRY(launch_attn_prefill(b.Q, w.key_cache, w.value_cache, T, pos0, c.n_heads, c.n_kv_heads, c.head_dim, b.O,
 		                        st));
@@ -185,7 +269,14 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 			e.x = b.X;
 			e.ldx = c.dim;
 			e.M = T;
-			TRY((launch_gemm<pf::EpiResidual, 1>(b.O, T, q_dim, one(w.wo, c.dim), one(w.wo, c.dim), c.dim, e, st)));
+			pf::E16Residual e16;
+			e16.x = b.X;
+			e16.ldx = c.dim;
+			e16.M = T;
+			bool done = false;
+			TRY(launch_g16_plain(g16_form(PG_WO), b.O, T, q_dim, one(w.wo, c.dim), c.dim, e16, st, done));
+			if (!done)
+				TRY((launch_gemm<pf::EpiResidual, 1>(b.O, T, q_dim, one(w.wo, c.dim), one(w.wo, c.dim), c.dim, e, st)));
 		}
 		pf::rmsnorm_rows_kernel<<<T, 256, 0, st>>>(b.X, w.rms_ffn, c.dim, c.norm_eps, b.Xn);
 		HIPCHK(hipGetLastError());
@@ -195,15 +286,39 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 			e.x = b.X;
 			e.ldx = c.dim;
 			e.M = T;
-			TRY((launch_gemm<pf::EpiResidual, 1>(b.H, T, c.hidden_dim, one(w.w2, c.dim), one(w.w2, c.dim), c.dim, e,
-			                                     st)));
+			pf::E16Residual e16;
+			e16.x = b.X;
+			e16.ldx = c.dim;
+			e16.M = T;
+			bool done = false;
+			TRY(launch_g16_plain(g16_form(PG_W2), b.H, T, c.hidden_dim, one(w.w2, c.dim), c.dim, e16, st, done));
+			if (!done)
+				TRY((launch_gemm<pf::EpiResidual, 1>(b.H, T, c.hidden_dim, one(w.w2, c.dim), one(w.w2, c.dim), c.dim, e,
+				                                     st)));
 		}
 	}
 	if (!want_lp)
 		return YALM_OK;
 	pf::rmsnorm_rows_kernel<<<T, 256, 0, st>>>(b.X, d->rms_final, c.dim, c.norm_eps, b.Xn);
 	HIPCHK(hipGetLastError());
-	const int ntiles = c.vocab_size / pf::BN;
+	const int cls_form = g16_form(PG_CLS);
+	const bool cls16 = cls_form && c.vocab_size % cls_form == 0;
+	const int ntiles = c.vocab_size / (cls16 ? cls_form : pf::BN);
+	if (cls16) {
+		pf::E16Logits e;
+		e.pmax = b.pmax;
+		e.psum = b.psum;
+		e.tgt_logit = b.tgt_logit;
+		e.targets = b.tgt;
+		e.M = T;
+		e.ntiles = ntiles;
+		e.red = nullptr;
+		bool done = false;
+		TRY(launch_g16_plain(cls_form, b.Xn, T, c.dim, one(d->wcls, c.vocab_size), c.vocab_size, e, st, done));
+		pf::logprob_kernel<<<T, 256, 0, st>>>(b.pmax, b.psum, b.tgt_logit, b.tgt, T, ntiles, b.lp);
+		HIPCHK(hipGetLastError());
+		return YALM_OK;
+	}
 	pf::EpiLogits e;
 	e.pmax = b.pmax;
 	e.psum = b.psum;
@@ -295,11 +410,18 @@ extern "C" int yalm_gemm_f16(float *c, const uint16_t *a, const uint16_t *w, int
 	TRY(hd(da, a, (size_t)M * K * 2));
 	TRY(hd(dw, w, (size_t)N * K * 2));
 	TRY(hd(dc, nullptr, (size_t)M * N * 4));
+	pf::E16StoreF32 e16;
+	e16.c = (float *)dc.p;
+	e16.ldc = N;
+	e16.M = M;
+	bool done = false;
+	TRY(launch_g16_plain(g16_form(PG_TEST), (const uint16_t *)da.p, M, K, one(dw.p, N), N, e16, nullptr, done));
 	pf::EpiStoreF32 e;
 	e.c = (float *)dc.p;
 	e.ldc = N;
 	e.M = M;
-	TRY((launch_gemm<pf::EpiStoreF32, 1>((const uint16_t *)da.p, M, K, one(dw.p, N), one(dw.p, N), N, e, nullptr)));
+	if (!done)
+		TRY((launch_gemm<pf::EpiStoreF32, 1>((const uint16_t *)da.p, M, K, one(dw.p, N), one(dw.p, N), N, e, nullptr)));
 	HIPCHK(hipDeviceSynchronize());
 	HIPCHK(hipMemcpy(c, dc.p, (size_t)M * N * 4, hipMemcpyDeviceToHost));
 	return YALM_OK;

@@ -1,0 +1,356 @@
+// prefill_gemm.h — the prefill's large-tile MFMA GEMM: C = A · W^T with a
+// 256-row output tile per workgroup and 8 waves, for the shapes where the
+// 128 x 128 tile of prefill.h (gemm_nt_kernel) is bound by LDS traffic.
+//
+// Why a bigger tile: an MFMA needs its A and B fragments read from LDS. With
+// the 128 x 128 tile each of the 4 waves owns 64 x 64 outputs and reads one
+// 1-KB fragment per 32x32x16 MFMA (4 reads per 4 MFMAs); the LDS-DMA fill of
+// the next K tile adds 32 KB per 64-deep step. Here each of the 8 waves owns
+// 128 x 64 (BN 256) or 64 x 64 (BN 128) outputs of a 256 x BN tile and issues
+// v_mfma_f32_16x16x32_f16: 12 fragment reads per 32 MFMAs (BN 256), and the
+// per-flop LDS-DMA traffic halves (cdna_hip_programming.md §5: the 256² tile is
+// the one that gets past the 128²-tile ceiling).
+//
+// Pipeline: two LDS buffers of one 64-deep K tile (A 32 KB + B BN x 128 B);
+// the LDS-DMA of tile kt + 1 (global_load_lds_dwordx4, XOR-swizzled source,
+// lane-linear LDS image) is issued before tile kt's MFMAs and waited for
+// (counted vmcnt(0), raw s_barrier) after them, so it has a whole tile of MFMA
+// time (2048 SIMD cycles at BN 256) to land from L2 / MALL. Two waves per SIMD:
+// one wave's fragment reads overlap the other's MFMAs.
+//
+// Operands: A [M][K] f16 (activations), W [N][K] f16 (.yalm [out][in] layout):
+// both K-contiguous, every fragment a 16-byte row read. B rows come from a
+// policy (BRowsPlain: up to 3 matrices end to end, the wq | wk | wv QKV;
+// BRowsGlu: W1 and W3 rows interleaved per wave so one wave holds W1 and W3
+// columns of the same 32 outputs). Accumulation f32; epilogues in the 16x16
+// C layout (column = lane & 15, row = 4 (lane >> 4) + reg).
+#pragma once
+
+#include "prefill.h"
+
+namespace pf {
+
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+constexpr int G_BM = 256, G_BK = 64, G_THREADS = 512;
+
+// C/D map of v_mfma_f32_16x16x32: column = lane & 15, row = 4 (lane >> 4) + reg.
+__device__ __forceinline__ int crow16(int reg, int lane) { return 4 * (lane >> 4) + reg; }
+
+// ---------------------------------------------------------------- B row policies
+struct BRowsPlain { // W rows n0 + r from up to 3 row-major [rows][K] matrices laid end to end
+	BSrc src;
+	static constexpr int COLS_PER_TILE_DIV = 1; // output columns per tile = BN
+	__device__ __forceinline__ const uint16_t *row(int n0, int r, int K) const {
+		const int n = n0 + r;
+		const int s = n < src.end[0] ? 0 : (n < src.end[1] ? 1 : 2);
+		const int start = s == 0 ? 0 : src.end[s - 1];
+		return src.p[s] + (size_t)(n - start) * K;
+	}
+};
+
+// GLU: a tile covers BN / 2 hidden columns h0 .. ; wave column wc's TN B rows are
+// TN / 2 W1 rows then the same TN / 2 W3 rows (h0 + wc * TN / 2 + ..).
+template <int TN>
+struct BRowsGlu {
+	const uint16_t *w1, *w3;
+	static constexpr int COLS_PER_TILE_DIV = 2;
+	__device__ __forceinline__ const uint16_t *row(int h0, int r, int K) const {
+		const int wc = r / TN, within = r % TN;
+		const int mat = within / (TN / 2);
+		const int hc = h0 + wc * (TN / 2) + within % (TN / 2);
+		return (mat ? w3 : w1) + (size_t)hc * K;
+	}
+};
+
+// ---------------------------------------------------------------- epilogues (16x16 layout)
+// apply(acc, m0, n0, lane): acc[FI][FJ] f32x4; element (i, j, r) is row
+// m0 + 16 i + crow16(r), column n0 + 16 j + (lane & 15) of the tile-local output.
+
+struct E16StoreF32 {
+	static constexpr bool NEEDS_LDS = false;
+	float *red = nullptr;
+	float *c;
+	int ldc, M;
+	template <int FI, int FJ>
+	__device__ __forceinline__ void apply(f32x4_t (&acc)[FI][FJ], int m0, int n0, int lane, int, int) const {
+#pragma unroll
+		for (int i = 0; i < FI; ++i)
+#pragma unroll
+			for (int r = 0; r < 4; ++r) {
+				const int m = m0 + 16 * i + crow16(r, lane);
+				if (m >= M)
+					continue;
+#pragma unroll
+				for (int j = 0; j < FJ; ++j)
+					c[(size_t)m * ldc + n0 + 16 * j + (lane & 15)] = acc[i][j][r];
+			}
+	}
+};
+
+struct E16Residual { // X[m][n] += C  (fused_matmul_add_residuals, per row)
+	static constexpr bool NEEDS_LDS = false;
+	float *red = nullptr;
+	float *x;
+	int ldx, M;
+	template <int FI, int FJ>
+	__device__ __forceinline__ void apply(f32x4_t (&acc)[FI][FJ], int m0, int n0, int lane, int, int) const {
+#pragma unroll
+		for (int i = 0; i < FI; ++i)
+#pragma unroll
+			for (int r = 0; r < 4; ++r) {
+				const int m = m0 + 16 * i + crow16(r, lane);
+				if (m >= M)
+					continue;
+#pragma unroll
+				for (int j = 0; j < FJ; ++j)
+					x[(size_t)m * ldx + n0 + 16 * j + (lane & 15)] += acc[i][j][r];
+			}
+	}
+};
+
+// H = f16(act(X W1^T) * (X W3^T)) (fused_ffn_w1_w3_glu_act): columns j < FJ / 2 of a
+// wave are W1 outputs, j >= FJ / 2 the W3 outputs of the same hidden columns.
+// n0 here is the wave's first HIDDEN column (BRowsGlu).
+template <int ACT>
+struct E16Glu {
+	static constexpr bool NEEDS_LDS = false;
+	float *red = nullptr;
+	uint16_t *h;
+	int ldh, M;
+	template <int FI, int FJ>
+	__device__ __forceinline__ void apply(f32x4_t (&acc)[FI][FJ], int m0, int n0, int lane, int, int) const {
+#pragma unroll
+		for (int i = 0; i < FI; ++i)
+#pragma unroll
+			for (int r = 0; r < 4; ++r) {
+				const int m = m0 + 16 * i + crow16(r, lane);
+				if (m >= M)
+					continue;
+#pragma unroll
+				for (int j = 0; j < FJ / 2; ++j)
+					h[(size_t)m * ldh + n0 + 16 * j + (lane & 15)] =
+					    f2h_bits(act_fn<ACT>(acc[i][j][r]) * acc[i][j + FJ / 2][r]);
+			}
+	}
+};
+
+// [q | k | v] columns: clip (infer.cpp:280-288), RoPE on (even, odd) column pairs =
+// lanes (l, l ^ 1) via DPP (infer.cpp:291-301), q -> f16 Q, k / v -> the fp16 cache
+// rows pos0 + m (fused_rope_and_cache_update, infer.cu:642-677); as EpiQKV.
+struct E16QKV {
+	static constexpr bool NEEDS_LDS = false;
+	float *red = nullptr;
+	uint16_t *q;
+	uint16_t *kc, *vc;
+	const float *rope;
+	int M, q_dim, kv_dim, head_dim, pos0;
+	float clip;
+	template <int FI, int FJ>
+	__device__ __forceinline__ void apply(f32x4_t (&acc)[FI][FJ], int m0, int n0, int lane, int, int) const {
+		const bool odd = lane & 1;
+#pragma unroll
+		for (int j = 0; j < FJ; ++j) {
+			const int n = n0 + 16 * j + (lane & 15);
+			const bool is_v = n >= q_dim + kv_dim;
+			const int nn = n < q_dim ? n : (n < q_dim + kv_dim ? n - q_dim : n - q_dim - kv_dim);
+			const int fj = (nn % head_dim) >> 1;
+#pragma unroll
+			for (int i = 0; i < FI; ++i)
+#pragma unroll
+				for (int r = 0; r < 4; ++r) {
+					float v = acc[i][j][r];
+					v = v < -clip ? -clip : (v > clip ? clip : v);
+					const float p = dpp<0xB1>(v); // partner column (n ^ 1)
+					const int m = m0 + 16 * i + crow16(r, lane);
+					if (m >= M)
+						continue;
+					const int pos = pos0 + m;
+					float o = v;
+					if (!is_v) {
+						const float2_t cs = *(const float2_t *)(rope + ((size_t)m * (head_dim >> 1) + fj) * 2);
+						o = odd ? p * cs[1] + v * cs[0] : v * cs[0] - p * cs[1];
+					}
+					if (n < q_dim)
+						q[(size_t)m * q_dim + n] = f2h_bits(o);
+					else if (!is_v)
+						kc[(size_t)pos * kv_dim + nn] = f2h(o);
+					else
+						vc[(size_t)pos * kv_dim + nn] = f2h(o);
+				}
+		}
+	}
+};
+
+// Per (row, BN-column tile): max and sum of exp over the tile's logits, and the
+// target token's logit when it falls in the tile (sample_prob, sampler.cpp:11-25,
+// split over vocab tiles; combined by logprob_kernel). Wave partials meet in LDS.
+struct E16Logits {
+	static constexpr bool NEEDS_LDS = true;
+	float *pmax, *psum, *tgt_logit;
+	const int *targets;
+	int M, ntiles;
+	float *red; // LDS scratch [WN][256 rows][2]
+	template <int FI, int FJ>
+	__device__ __forceinline__ void apply(f32x4_t (&acc)[FI][FJ], int m0, int n0, int lane, int wc, int wn) const {
+		const int tm0 = m0 - (m0 % G_BM); // tile's first row
+#pragma unroll
+		for (int i = 0; i < FI; ++i) {
+#pragma unroll
+			for (int r = 0; r < 4; ++r) {
+				const int m = m0 + 16 * i + crow16(r, lane);
+				const int tgt = m < M ? targets[m] : -1;
+				float mx = acc[i][0][r];
+#pragma unroll
+				for (int j = 1; j < FJ; ++j)
+					mx = fmaxf(mx, acc[i][j][r]);
+				mx = row16_max(mx); // the 16 lanes of this row group hold its 16 columns
+#pragma unroll
+				for (int j = 0; j < FJ; ++j)
+					if (n0 + 16 * j + (lane & 15) == tgt)
+						tgt_logit[m] = acc[i][j][r];
+				float s = 0.0f;
+#pragma unroll
+				for (int j = 0; j < FJ; ++j)
+					s += expf(acc[i][j][r] - mx);
+				s = row16_sum(s);
+				if ((lane & 15) == 0) {
+					const int rl = m - tm0;
+					red[(wc * G_BM + rl) * 2 + 0] = mx;
+					red[(wc * G_BM + rl) * 2 + 1] = s;
+				}
+			}
+		}
+		__syncthreads();
+		for (int row = threadIdx.x; row < G_BM; row += G_THREADS) {
+			const int m = tm0 + row;
+			if (m >= M)
+				continue;
+			float mx = -FLT_MAX;
+			for (int w = 0; w < wn; ++w)
+				mx = fmaxf(mx, red[(w * G_BM + row) * 2]);
+			float s = 0.0f;
+			for (int w = 0; w < wn; ++w)
+				s += red[(w * G_BM + row) * 2 + 1] * expf(red[(w * G_BM + row) * 2] - mx);
+			const int tile = n0 / (16 * FJ * wn); // n0 of wave 0 ... any wave: tile = column tile index
+			pmax[(size_t)m * ntiles + tile] = mx;
+			psum[(size_t)m * ntiles + tile] = s;
+		}
+	}
+};
+
+// ---------------------------------------------------------------- the kernel
+// Stage ROWS x 64 f16 of one operand into a lane-linear LDS image by LDS-DMA: wave
+// instruction = 8 rows x 128 B; lane l writes row 8 rb + (l >> 3), chunk l & 7 and
+// reads source chunk (l & 7) ^ (row & 7) (the swizzle lives on the source address;
+// g16frag applies the same involution on the read). rowp[i]: this lane's row base of
+// instruction i (already clamped / mapped).
+template <int NI>
+__device__ __forceinline__ void g16stage(uint16_t *lds, const uint16_t *const (&rowp)[NI], int k0, int wave, int lane) {
+#pragma unroll
+	for (int i = 0; i < NI; ++i) {
+		const int rb = wave * NI + i;
+		const int r = rb * 8 + (lane >> 3);
+		const int c = lane & 7;
+		__builtin_amdgcn_global_load_lds((const void *)(rowp[i] + k0 + 8 * (c ^ (r & 7))),
+		                                 (YALM_LDS void *)(lds + rb * 8 * G_BK), 16, 0, 0);
+	}
+}
+
+// 16x16x32 operand fragment: tile row r, k-step s (32 deep): lane group q = lane >> 4
+// holds k = 32 s + 8 q .. + 7 (cdna_hip_programming.md §3 16x16x32 A/B maps).
+__device__ __forceinline__ half8_t g16frag(const uint16_t *lds, int r, int s, int lane) {
+	const int kc = 4 * s + (lane >> 4);
+	return *(const half8_t *)(lds + r * G_BK + 8 * (kc ^ (r & 7)));
+}
+
+// C tile [256][BN] of C = A · B^T, B rows through BMAP. 8 waves as WM x (8 / WM).
+template <class EPI, class BMAP, int BN, int WM>
+__global__ __launch_bounds__(G_THREADS, 1) void gemm16_kernel(const uint16_t *__restrict__ A, int M, int K, BMAP bm,
+                                                             int N, EPI epi) {
+	constexpr int WN = 8 / WM;
+	constexpr int TM = G_BM / WM, TN = BN / WN; // per-wave output
+	constexpr int FI = TM / 16, FJ = TN / 16;
+	constexpr int NIA = G_BM / 8 / 8, NIB = BN / 8 / 8; // LDS-DMA instructions per thread and operand
+	constexpr int TA = G_BM * G_BK, TB = BN * G_BK;    // f16 per operand tile
+	constexpr int BUF = TA + TB;
+	extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+	const int lane = threadIdx.x & 63;
+	const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	const int wr = wave / WN, wc = wave % WN;
+
+	// XCD-aware tile order (bijective remap, cdna_hip_programming.md §5 'XCD swizzle'):
+	// the workgroups sharing an XCD walk down M for fixed column panels (B reused in L2)
+	const int tiles_m = (M + G_BM - 1) / G_BM, tiles_n = N / BN;
+	const int nwg = tiles_m * tiles_n;
+	int wg = blockIdx.x;
+	{
+		const int q = nwg / 8, rr = nwg % 8, xcd = wg % 8, idx = wg / 8;
+		wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
+	}
+	const int tm = wg % tiles_m, tn = wg / tiles_m;
+	const int row0 = tm * G_BM;
+	const int colB = tn * (BN / BMAP::COLS_PER_TILE_DIV); // first B column (plain) / hidden column (GLU)
+
+	const uint16_t *ap[NIA], *bp[NIB];
+#pragma unroll
+	for (int i = 0; i < NIA; ++i)
+		ap[i] = A + (size_t)min(row0 + (wave * NIA + i) * 8 + (lane >> 3), M - 1) * K;
+#pragma unroll
+	for (int i = 0; i < NIB; ++i)
+		bp[i] = bm.row(colB, (wave * NIB + i) * 8 + (lane >> 3), K);
+
+	f32x4_t acc[FI][FJ];
+#pragma unroll
+	for (int i = 0; i < FI; ++i)
+#pragma unroll
+		for (int j = 0; j < FJ; ++j)
+			acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+	const int nk = K / G_BK;
+	auto stage = [&](int buf, int kt) {
+		uint16_t *base = smem + buf * BUF;
+		g16stage<NIA>(base, ap, kt * G_BK, wave, lane);
+		g16stage<NIB>(base + TA, bp, kt * G_BK, wave, lane);
+	};
+	stage(0, 0);
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	raw_barrier();
+	for (int kt = 0; kt < nk; ++kt) {
+		if (kt + 1 < nk)
+			stage((kt + 1) & 1, kt + 1); // that buffer's last readers passed the previous barrier
+		const uint16_t *sa = smem + (kt & 1) * BUF;
+		const uint16_t *sb = sa + TA;
+#pragma unroll
+		for (int s = 0; s < G_BK / 32; ++s) {
+			half8_t af[FI], bf[FJ];
+#pragma unroll
+			for (int j = 0; j < FJ; ++j)
+				bf[j] = g16frag(sb, wc * TN + 16 * j + (lane & 15), s, lane);
+#pragma unroll
+			for (int i = 0; i < FI; ++i)
+				af[i] = g16frag(sa, wr * TM + 16 * i + (lane & 15), s, lane);
+			__builtin_amdgcn_s_setprio(1);
+#pragma unroll
+			for (int i = 0; i < FI; ++i)
+#pragma unroll
+				for (int j = 0; j < FJ; ++j)
+					acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+			__builtin_amdgcn_s_setprio(0);
+		}
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // tile kt + 1 landed (this thread's DMAs)
+		raw_barrier();                                     // ... everyone's; everyone done reading tile kt
+	}
+	EPI e = epi;
+	if constexpr (EPI::NEEDS_LDS)
+		e.red = (float *)smem; // the staging buffers are free after the last barrier
+	const int n0 = BMAP::COLS_PER_TILE_DIV == 1 ? colB + wc * TN : colB + wc * (TN / 2);
+	e.template apply<FI, FJ>(acc, row0 + wr * TM, n0, lane, wc, WN);
+}
+
+template <int BN>
+constexpr size_t gemm16_lds() {
+	return (size_t)2 * (G_BM + BN) * G_BK * sizeof(uint16_t);
+}
+
+} // namespace pf
