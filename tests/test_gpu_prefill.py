@@ -48,7 +48,8 @@ FORMS = {"auto": {}, "s2": {"YALM_PF_STAGES": "2", "YALM_PF_G16": "0"}, "s3": {"
          "s3-wide": {"YALM_PF_STAGES": "3", "YALM_PF_WIDE": "1", "YALM_PF_G16": "0"},
          "s2-wide": {"YALM_PF_STAGES": "2", "YALM_PF_WIDE": "1", "YALM_PF_G16": "0"},
          "s3-narrow": {"YALM_PF_STAGES": "3", "YALM_PF_WIDE": "0", "YALM_PF_G16": "0"},
-         "g16-256": {"YALM_PF_G16": G16_ALL.format(256)}, "g16-128": {"YALM_PF_G16": G16_ALL.format(128)}}
+         "g16-256": {"YALM_PF_G16": G16_ALL.format(256)}, "g16-128": {"YALM_PF_G16": G16_ALL.format(128)},
+         "g16-192": {"YALM_PF_G16": G16_ALL.format(192)}, "g16-320": {"YALM_PF_G16": G16_ALL.format(320)}}
 
 
 @pytest.mark.parametrize("form", list(FORMS))
@@ -119,16 +120,20 @@ CFGS = {
     "small-d64": M.SMALL,
     "gqa-d128": M.ModelConfig(dim=512, hidden_dim=1024, head_dim=128, n_layers=3, n_heads=4, n_kv_heads=2,
                               vocab_size=1024, max_seq_len=320, rope_theta=1e6, act=M.SILU, weight_dtype=M.F16),
+    # QKV N 1280 = 4 x 320, Wo / W2 N 768 = 4 x 192, vocab 1920 = 10 x 192: the 192 / 320 tile widths
+    "d768": M.ModelConfig(dim=768, hidden_dim=1536, head_dim=128, n_layers=2, n_heads=6, n_kv_heads=2,
+                          vocab_size=1920, max_seq_len=320, rope_theta=1e6, act=M.SILU, weight_dtype=M.F16),
 }
 
 
-@pytest.mark.parametrize("form", ["auto", "s3", "s2-wide", "g16-256", "g16-128"])
-def test_prefill_forms_match_decode(form, monkeypatch):
+@pytest.mark.parametrize("cfg_name", ["gqa-d128", "d768"])
+@pytest.mark.parametrize("form", ["auto", "s3", "s2-wide", "g16-256", "g16-128", "g16-192", "g16-320"])
+def test_prefill_forms_match_decode(form, cfg_name, monkeypatch):
     """The whole prefill in each GEMM form (the wide tile on every GEMM with N %
     256 == 0, incl. the vocab-tiled logits epilogue run once per column half)."""
     for k, v in FORMS[form].items():
         monkeypatch.setenv(k, v)
-    cfg = CFGS["gqa-d128"]
+    cfg = CFGS[cfg_name]
     R = rt()
     dm = R.DeviceModel.synthetic(cfg, seed=4)
     tokens = np.random.default_rng(5).integers(0, cfg.vocab_size, size=90).astype(np.int32)

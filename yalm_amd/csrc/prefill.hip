@@ -64,14 +64,17 @@ int launch_gemm(const uint16_t *A, int M, int K, pf::BSrc b0, pf::BSrc b1, int N
 	return YALM_OK;
 }
 
-// Large-tile GEMM form per GEMM kind (prefill_gemm.h): 0 = the 128 x 128 kernel,
-// 256 / 128 = gemm16_kernel with a 256 x BN tile. YALM_PF_G16 = "qkv:256,wo:128,..."
-// overrides (read per launch: tests switch it inside one process).
+// Large-tile GEMM form per GEMM kind (prefill_gemm.h): the tile width BN of
+// gemm16_kernel (256 rows x BN columns), 0 = the 128 x 128 kernel of prefill.h.
+// Default: auto -- the BN dividing N that minimises rounds x (BN + 64), rounds =
+// ceil(tiles / CUs): a 256-CU chip should get whole rounds of large tiles (Llama-3B
+// QKV N 5120 -> 320: 256 tiles at T 4096 instead of 320; Wo / W2 N 3072 -> 192).
+// YALM_PF_G16 = "qkv:256,wo:128,..." forces a width, "0" (or kind:0) the old kernel
+// (read per launch: tests switch it inside one process).
 enum { PG_QKV = 0, PG_WO = 1, PG_GLU = 2, PG_W2 = 3, PG_CLS = 4, PG_TEST = 5 };
 int g16_form(int kind) {
-	static const int defaults[6] = {256, 128, 256, 128, 256, 256};
 	static const char *names[6] = {"qkv", "wo", "glu", "w2", "cls", "test"};
-	int f = defaults[kind];
+	int f = -1; // auto
 	if (const char *e = getenv("YALM_PF_G16")) {
 		if (!strcmp(e, "0"))
 			return 0;
@@ -79,7 +82,34 @@ int g16_form(int kind) {
 		if (p && p[strlen(names[kind])] == ':')
 			f = atoi(p + strlen(names[kind]) + 1);
 	}
-	return f == 256 || f == 128 ? f : 0;
+	return f;
+}
+
+// BN for a GEMM of M x N (n_eff = B rows: 2 x hidden for the GLU); 0 = none fits
+int pick_bn(int form, int M, int n_eff, bool glu) {
+	static const int cands[4] = {128, 192, 256, 320};
+	if (form == 0)
+		return 0;
+	if (form > 0) {
+		const bool ok = n_eff % form == 0 && (!glu || form == 128 || form == 256) &&
+		                (form == 128 || form == 192 || form == 256 || form == 320);
+		return ok ? form : 0;
+	}
+	const long ncu = device_cu_count();
+	const long tiles_m = (M + pf::G_BM - 1) / pf::G_BM;
+	int best = 0;
+	long best_cost = 0;
+	for (int bn : cands) {
+		if (n_eff % bn || (glu && bn != 128 && bn != 256))
+			continue;
+		const long rounds = (tiles_m * (n_eff / bn) + ncu - 1) / ncu;
+		const long cost = rounds * (bn + 64);
+		if (!best || cost < best_cost || (cost == best_cost && bn > best)) {
+			best = bn;
+			best_cost = cost;
+		}
+	}
+	return best;
 }
 
 template <class EPI, class BMAP, int BN, int WM>
@@ -97,21 +127,24 @@ int launch_g16_t(const uint16_t *A, int M, int K, const BMAP &bm, int N, const E
 	return YALM_OK;
 }
 
-// C = A · W^T through the large-tile kernel when the form allows (N % BN == 0),
-// else false (the caller launches gemm_nt_kernel).
+// C = A · W^T through the large-tile kernel at width bn (pick_bn); done = false
+// when bn is 0 (the caller launches gemm_nt_kernel).
 template <class EPI>
-int launch_g16_plain(int form, const uint16_t *A, int M, int K, const pf::BSrc &b, int N, const EPI &epi,
+int launch_g16_plain(int bn, const uint16_t *A, int M, int K, const pf::BSrc &b, int N, const EPI &epi,
                      hipStream_t st, bool &done) {
-	done = false;
 	pf::BRowsPlain bm{b};
-	if (form == 256 && N % 256 == 0) {
-		done = true;
-		return launch_g16_t<EPI, pf::BRowsPlain, 256, 2>(A, M, K, bm, N, epi, st);
-	}
-	if (form == 128 && N % 128 == 0) {
-		done = true;
+	done = true;
+	switch (bn) {
+	case 128:
 		return launch_g16_t<EPI, pf::BRowsPlain, 128, 4>(A, M, K, bm, N, epi, st);
+	case 192:
+		return launch_g16_t<EPI, pf::BRowsPlain, 192, 2>(A, M, K, bm, N, epi, st);
+	case 256:
+		return launch_g16_t<EPI, pf::BRowsPlain, 256, 2>(A, M, K, bm, N, epi, st);
+	case 320:
+		return launch_g16_t<EPI, pf::BRowsPlain, 320, 2>(A, M, K, bm, N, epi, st);
 	}
+	done = false;
 	return YALM_OK;
 }
 
@@ -187,18 +220,16 @@ int ensure_bufs(yalm_decoder_s *d) {
 template <int ACT>
 int enqueue_glu(yalm_decoder_s *d, const yalm_block_weights &w, int T) {
 	const yalm_config &c = d->c;
-	const int form = g16_form(PG_GLU);
-	if (form && c.hidden_dim % (form / 2) == 0) {
+	const int bn = pick_bn(g16_form(PG_GLU), T, 2 * c.hidden_dim, true);
+	if (bn) {
 		pf::E16Glu<ACT> e;
 		e.h = d->pf.H;
 		e.ldh = c.hidden_dim;
 		e.M = T;
-		if (form == 256) {
-			pf::BRowsGlu<64> bm{(const uint16_t *)w.w1, (const uint16_t *)w.w3};
+		pf::BRowsGlu<64> bm{(const uint16_t *)w.w1, (const uint16_t *)w.w3};
+		if (bn == 256)
 			return launch_g16_t<pf::E16Glu<ACT>, pf::BRowsGlu<64>, 256, 2>(d->pf.Xn, T, c.dim, bm, 2 * c.hidden_dim,
 			                                                             e, d->stream);
-		}
-		pf::BRowsGlu<64> bm{(const uint16_t *)w.w1, (const uint16_t *)w.w3};
 		return launch_g16_t<pf::E16Glu<ACT>, pf::BRowsGlu<64>, 128, 4>(d->pf.Xn, T, c.dim, bm, 2 * c.hidden_dim, e,
 		                                                             d->stream);
 	}
@@ -246,7 +277,8 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 				e.head_dim = c.head_dim;
 				e.pos0 = pos0;
 				e.clip = c.qkv_clip;
-				TRY(launch_g16_plain(g16_form(PG_QKV), b.Xn, T, c.dim, qkv, q_dim + 2 * kv_dim, e, st, done));
+				TRY(launch_g16_plain(pick_bn(g16_form(PG_QKV), T, q_dim + 2 * kv_dim, false), b.Xn, T, c.dim, qkv,
+				                     q_dim + 2 * kv_dim, e, st, done));
 			}
 			pf::EpiQKV e;
 			e.q = b.Q;
@@ -274,7 +306,8 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 			e16.ldx = c.dim;
 			e16.M = T;
 			bool done = false;
-			TRY(launch_g16_plain(g16_form(PG_WO), b.O, T, q_dim, one(w.wo, c.dim), c.dim, e16, st, done));
+			TRY(launch_g16_plain(pick_bn(g16_form(PG_WO), T, c.dim, false), b.O, T, q_dim, one(w.wo, c.dim), c.dim, e16,
+			                     st, done));
 			if (!done)
 				TRY((launch_gemm<pf::EpiResidual, 1>(b.O, T, q_dim, one(w.wo, c.dim), one(w.wo, c.dim), c.dim, e, st)));
 		}
@@ -291,7 +324,8 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 			e16.ldx = c.dim;
 			e16.M = T;
 			bool done = false;
-			TRY(launch_g16_plain(g16_form(PG_W2), b.H, T, c.hidden_dim, one(w.w2, c.dim), c.dim, e16, st, done));
+			TRY(launch_g16_plain(pick_bn(g16_form(PG_W2), T, c.dim, false), b.H, T, c.hidden_dim, one(w.w2, c.dim), c.dim,
+			                     e16, st, done));
 			if (!done)
 				TRY((launch_gemm<pf::EpiResidual, 1>(b.H, T, c.hidden_dim, one(w.w2, c.dim), one(w.w2, c.dim), c.dim, e,
 				                                     st)));
@@ -301,9 +335,9 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 		return YALM_OK;
 	pf::rmsnorm_rows_kernel<<<T, 256, 0, st>>>(b.X, d->rms_final, c.dim, c.norm_eps, b.Xn);
 	HIPCHK(hipGetLastError());
-	const int cls_form = g16_form(PG_CLS);
-	const bool cls16 = cls_form && c.vocab_size % cls_form == 0;
-	const int ntiles = c.vocab_size / (cls16 ? cls_form : pf::BN);
+	const int cls_bn = pick_bn(g16_form(PG_CLS), T, c.vocab_size, false);
+	const bool cls16 = cls_bn != 0;
+	const int ntiles = c.vocab_size / (cls16 ? cls_bn : pf::BN);
 	if (cls16) {
 		pf::E16Logits e;
 		e.pmax = b.pmax;
@@ -314,7 +348,7 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 		e.ntiles = ntiles;
 		e.red = nullptr;
 		bool done = false;
-		TRY(launch_g16_plain(cls_form, b.Xn, T, c.dim, one(d->wcls, c.vocab_size), c.vocab_size, e, st, done));
+		TRY(launch_g16_plain(cls_bn, b.Xn, T, c.dim, one(d->wcls, c.vocab_size), c.vocab_size, e, st, done));
 		pf::logprob_kernel<<<T, 256, 0, st>>>(b.pmax, b.psum, b.tgt_logit, b.tgt, T, ntiles, b.lp);
 		HIPCHK(hipGetLastError());
 		return YALM_OK;
@@ -415,7 +449,8 @@ extern "C" int yalm_gemm_f16(float *c, const uint16_t *a, const uint16_t *w, int
 	e16.ldc = N;
 	e16.M = M;
 	bool done = false;
-	TRY(launch_g16_plain(g16_form(PG_TEST), (const uint16_t *)da.p, M, K, one(dw.p, N), N, e16, nullptr, done));
+	TRY(launch_g16_plain(pick_bn(g16_form(PG_TEST), M, N, false), (const uint16_t *)da.p, M, K, one(dw.p, N), N, e16,
+	                     nullptr, done));
 	pf::EpiStoreF32 e;
 	e.c = (float *)dc.p;
 	e.ldc = N;
