@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--tp-transport", default="rccl", choices=["rccl", "ipc"],
                     help="all-reduce transport for tensor parallelism: RCCL (one rank per GPU) or the IPC one-shot exchange")
     ap.add_argument("--no-envelope", action="store_true")
+    ap.add_argument("--no-alt", action="store_true",
+                    help="N > 1 over RCCL: skip the second measurement through the IPC exchange")
     ap.add_argument("--no-gpu-state", action="store_true",
                     help="skip the rocm-smi query (under a profiler: its preload would run inside rocm-smi too)")
     return ap.parse_args()
@@ -279,38 +281,44 @@ def main():
     tp = mode.startswith("tp-")
     tp_size = world if tp else 1
 
-    prompt = [(7 * i + 1) % cfg.vocab_size for i in range(PROMPT_LEN)]
-    for pos, t in enumerate(prompt[:-1]):
-        dec.forward(t, pos, runtime.HYDRATE_KV_CACHE)
-    # first generated token; the device loop continues from there
-    dec.generate_greedy(prompt[-1], PROMPT_LEN - 1, 1)
-    if args.warmup:
-        dec.enqueue_greedy(args.warmup)
-    runtime.check(runtime.lib.yalm_stream_sync(None))
-    _, pos0 = dec.device_step()
-
-    def barrier_sync():
+    def timed_decode(dec, tp):
+        """Hydrate the prompt, warm up, then time exactly args.steps greedy tokens
+        between barrier + sync points; (max-over-ranks seconds, pos0, pos1, ranks agree)."""
+        prompt = [(7 * i + 1) % cfg.vocab_size for i in range(PROMPT_LEN)]
+        for pos, t in enumerate(prompt[:-1]):
+            dec.forward(t, pos, runtime.HYDRATE_KV_CACHE)
+        # first generated token; the device loop continues from there
+        dec.generate_greedy(prompt[-1], PROMPT_LEN - 1, 1)
+        if args.warmup:
+            dec.enqueue_greedy(args.warmup)
         runtime.check(runtime.lib.yalm_stream_sync(None))
-        dec.device_step()  # syncs the decoder stream
-        if dist is not None:
-            dist.barrier()
+        _, pos0 = dec.device_step()
 
-    barrier_sync()
-    t0 = time.perf_counter()
-    dec.enqueue_greedy(args.steps)
-    dec.device_step()
-    t1 = time.perf_counter()
-    barrier_sync()
-    elapsed = t1 - t0
-    tok1, pos1 = dec.device_step()
-    assert pos1 - pos0 == args.steps, (pos0, pos1)
-    agree = None
-    if dist is not None:
-        allv = [None] * world
-        dist.all_gather_object(allv, (elapsed, tok1))
-        elapsed = max(v[0] for v in allv)
-        if tp:  # every rank must have produced the same token sequence
-            agree = len({v[1] for v in allv}) == 1
+        def barrier_sync():
+            runtime.check(runtime.lib.yalm_stream_sync(None))
+            dec.device_step()  # syncs the decoder stream
+            if dist is not None:
+                dist.barrier()
+
+        barrier_sync()
+        t0 = time.perf_counter()
+        dec.enqueue_greedy(args.steps)
+        dec.device_step()
+        t1 = time.perf_counter()
+        barrier_sync()
+        elapsed = t1 - t0
+        tok1, pos1 = dec.device_step()
+        assert pos1 - pos0 == args.steps, (pos0, pos1)
+        agree = None
+        if dist is not None:
+            allv = [None] * world
+            dist.all_gather_object(allv, (elapsed, tok1))
+            elapsed = max(v[0] for v in allv)
+            if tp:  # every rank must have produced the same token sequence
+                agree = len({v[1] for v in allv}) == 1
+        return elapsed, pos0, pos1, agree
+
+    elapsed, pos0, pos1, agree = timed_decode(dec, tp)
 
     # ---- roofline of the dominant kernel: the W1/W3 GEMV + SiLU-GLU (52.9% of the bytes)
     wb = M.DTYPE_BYTES[cfg.weight_dtype]
@@ -403,6 +411,19 @@ def main():
         out["fallback"] = fallback
     dec.close()
     dm.close()
+    if mode == "tp-rccl" and world > 1 and not args.no_alt:
+        # the same workload through the IPC one-shot exchange (include/yalm_hip.h), for
+        # the all-reduce cost of RCCL's collective vs direct peer-mapped stores
+        try:
+            dm, dec = make_decoder(runtime, M, cfg, rank, world, "tp-ipc", dist)
+            e2, _, _, agree2 = timed_decode(dec, True)
+            ex2 = dec.time_kernel(6, args.kernel_iters) * 1e3
+            out["tp_ipc"] = {"value": round(args.steps / e2, 3), "ms_per_step": round(e2 / args.steps * 1e3, 4),
+                             "exchange_us": round(ex2, 3), "ranks_agree": agree2}
+            dec.close()
+            dm.close()
+        except Exception as e:  # report, never hide
+            out["tp_ipc"] = {"error": str(e)[:200]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
