@@ -165,9 +165,11 @@ const char *yalm_kernel_name(yalm_decoder d, int kernel_id);
  * attention output is handed to the Wo workgroups as {value, epoch} granules. */
 int yalm_decoder_attn_wo(yalm_decoder d);
 /* Timeline of the most recent fused attention + Wo launch (decoder created with
- * YALM_ATTN_WO_TRACE=1): 4 s_memrealtime (100 MHz) stamps per workgroup at
- * [w * 4 + k]: start, hand-off signalled (attention; 0 if this workgroup did not
- * finish a kv head) or Wo slice landed (Wo; the trace waits for it), poll passed (Wo), end. Workgroups
+ * YALM_ATTN_WO_TRACE=1): 16 stamps per workgroup at [w * 16 + k]: k < 8
+ * s_memrealtime (100 MHz), k + 8 the shader clock (s_memtime) at the same point; k = 0 start, 1 hand-off signalled (attention; 0 if this workgroup did not
+ * finish a kv head) or Wo slice landed (Wo; the trace waits for it), 2 poll passed (Wo) or
+ * first K/V/q loads landed (attention; the trace waits for them), 3 end; attention only:
+ * 4 scores in LDS, 5 softmax done, 6 P.V partials in LDS, 7 merger's gather done. Workgroups
  * [0, *attention_workgroups) are attention, the rest Wo. */
 int yalm_attn_wo_trace(yalm_decoder d, unsigned long long *host, size_t count, int *workgroups,
                        int *attention_workgroups);

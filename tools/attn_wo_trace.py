@@ -38,6 +38,8 @@ def main():
     dec.forward(5, args.ctx)
     tr, na = dec.attn_wo_trace()
     tr = tr.astype(np.int64)
+    clk = tr[:, 8:]
+    tr = tr[:, :8]
     t0 = tr[:, 0].min()
     us = (tr - t0) / 100.0
     att, wo = us[:na], us[na:]
@@ -46,11 +48,29 @@ def main():
           f"launch span {us[:, 3].max():.2f} us")
     print(f"attention start  {q(att[:, 0])}")
     print(f"attention end    {q(att[:, 3])}")
+    active = att[tr[:na, 2] > 0]
+    print(f"active attention workgroups: {len(active)}")
+    print(f"  loads landed   {q(active[:, 2])}")
+    print(f"  scores in LDS  {q(active[:, 4])}")
+    print(f"  softmax done   {q(active[:, 5])}")
+    print(f"  P.V in LDS     {q(active[:, 6])}")
+    a_tr, a_clk = tr[:na][tr[:na, 2] > 0], clk[:na][tr[:na, 2] > 0]
+    for k0, k1, name in ((2, 4, "loads->scores"), (4, 5, "scores->softmax"), (5, 6, "softmax->P.V"), (6, 1, "P.V->signal")):
+        dt = (a_tr[:, k1] - a_tr[:, k0]) / 100.0
+        dc = a_clk[:, k1] - a_clk[:, k0]
+        print(f"  {name:16s} {np.median(dt):6.2f} us  {np.median(dc):8.0f} shader clocks  ({np.median(dc) / np.maximum(np.median(dt), 1e-3) / 1e3:5.2f} GHz)")
+    mergers = att[tr[:na, 7] > 0]
+    if len(mergers):
+        print(f"  merger gathered {q(mergers[:, 7])}  ({len(mergers)} mergers)")
     print(f"head signalled   {q(writers[:, 1])}  ({len(writers)} writers)")
     print(f"Wo start         {q(wo[:, 0])}")
     print(f"Wo slice landed  {q(wo[:, 1])}")
     print(f"Wo poll passed   {q(wo[:, 2])}")
     print(f"Wo end           {q(wo[:, 3])}")
+    w_tr, w_clk = tr[na:], clk[na:]
+    dt = (w_tr[:, 3] - w_tr[:, 2]) / 100.0
+    dc = w_clk[:, 3] - w_clk[:, 2]
+    print(f"  Wo poll->end     {np.median(dt):6.2f} us  {np.median(dc):8.0f} shader clocks")
     dec.close()
     dm.close()
 

@@ -89,15 +89,105 @@ __device__ __forceinline__ void attn_out_rep(float *out, size_t i, float v, unsi
 	}
 }
 
+// Sum over each aligned group of LPK lanes (one K row's pieces, LPK = head_dim / 8
+// in 2..32), result in every lane of the group: xor-butterfly of DPP quad_perm
+// [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror, then a lane swap across rows.
+template <int LPK>
+__device__ __forceinline__ float attn_row_sum(float v) {
+	if constexpr (LPK >= 2)
+		v += dpp<0xB1>(v);
+	if constexpr (LPK >= 4)
+		v += dpp<0x4E>(v);
+	if constexpr (LPK >= 8)
+		v += dpp<0x141>(v);
+	if constexpr (LPK >= 16)
+		v += dpp<0x140>(v);
+	if constexpr (LPK >= 32)
+		v += xor16(v);
+	return v;
+}
+// Sum / max over the row groups inside each DPP row, lane by lane (a lane meets
+// the lanes of the same piece, or of the same head when LPK is the head count):
+// row_ror by LPK, 2 LPK, .. 8.
+template <int LPK, bool MAX>
+__device__ __forceinline__ float attn_fold_row(float v) {
+	auto op = [](float a, float b) { return MAX ? fmaxf(a, b) : a + b; };
+	if constexpr (LPK <= 1)
+		v = op(v, dpp<0x121>(v));
+	if constexpr (LPK <= 2)
+		v = op(v, dpp<0x122>(v));
+	if constexpr (LPK <= 4)
+		v = op(v, dpp<0x124>(v));
+	if constexpr (LPK <= 8)
+		v = op(v, dpp<0x128>(v));
+	return v;
+}
+// One halving step of a 16-lane reduce-scatter over J groups of R values: the lane
+// keeps the upper or lower half of each group and adds its partner's copy of it
+// (CTRL: a DPP involution pairing lanes with opposite `upper`).
+template <int CTRL, int J, int R>
+__device__ __forceinline__ void attn_rs_step(const float (&in)[J * R], float (&out)[J * R / 2], bool upper) {
+	constexpr int H = R / 2;
+#pragma unroll
+	for (int j = 0; j < J; ++j)
+#pragma unroll
+		for (int k = 0; k < H; ++k) {
+			const float lo = in[j * R + k], hi = in[j * R + H + k];
+			out[j * H + k] = (upper ? hi : lo) + dpp<CTRL>(upper ? lo : hi);
+		}
+}
+// Lane r's value broadcast to its whole DPP row (row_newbcast:r, gfx90a+); r must
+// fold to a constant once the caller's loops are unrolled.
+__device__ __forceinline__ float row_bcast16(float v, int r) {
+	switch (r) {
+	case 0: return dpp<0x150>(v);
+	case 1: return dpp<0x151>(v);
+	case 2: return dpp<0x152>(v);
+	case 3: return dpp<0x153>(v);
+	case 4: return dpp<0x154>(v);
+	case 5: return dpp<0x155>(v);
+	case 6: return dpp<0x156>(v);
+	case 7: return dpp<0x157>(v);
+	case 8: return dpp<0x158>(v);
+	case 9: return dpp<0x159>(v);
+	case 10: return dpp<0x15A>(v);
+	case 11: return dpp<0x15B>(v);
+	case 12: return dpp<0x15C>(v);
+	case 13: return dpp<0x15D>(v);
+	case 14: return dpp<0x15E>(v);
+	default: return dpp<0x15F>(v);
+	}
+}
+// Max / sum over all the wave's row groups of a value every lane of a group holds.
+template <int LPK, bool MAX>
+__device__ __forceinline__ float attn_wave_red(float v) {
+	auto op = [](float a, float b) { return MAX ? fmaxf(a, b) : a + b; };
+	v = attn_fold_row<LPK, MAX>(v);
+	if constexpr (LPK <= 16)
+		v = op(v, xor16(v));
+	return op(v, xor32(v));
+}
+
 // One workgroup's share of the split-KV attention: kv head g, key chunks s0,
 // s0 + S, ... `hook()` runs right after the speculative K/V and q loads are
 // issued (attn_wo.h issues its weight stream there, behind them in vmcnt order).
 // Returns true on the workgroup that wrote the final head outputs of kv head g
 // (the single-chunk writer or the merger); the result is workgroup-uniform.
-// D = head_dim (multiple of 8, D/8 a power of two <= 64); GT >= G.
+// D = head_dim (16 .. 256, a power of two); GT >= G.
 // GRAN: outputs as {value, gtag} granules into `out` read as unsigned long long[].
 // part: [n_heads][nsplit][D + 2] granules tagged ptag (attn_part_tag); err: bit 2
 // set if the merger's bounded wait gave up (results wrong, reported).
+// ts / trace_on: attn_wo.h's timeline stamps (thread 0) and the trace-only waits.
+//
+// Round 4 layout: each wave runs its 16 keys of the chunk to the end WITHOUT a
+// workgroup barrier -- lane (row group, piece) holds 8 dims of NK K/V rows; the
+// scores are reduced across the row's pieces with DPP, the softmax statistics
+// are per wave (max / sum across row groups with DPP and lane swaps), P is never
+// stored, and the P.V sums are reduced across row groups in registers (transposed
+// sum4_rows). One barrier per chunk then combines the 4 waves' (m, l, o) with
+// the flash-decoding rescaling. Round 3 staged the partial dots, the scores and
+// the P.V partials through LDS behind 4 barriers (~6700 shader clocks from the
+// loads landing to the head outputs; tools/attn_wo_trace.py).
 template <int D, int GT, bool GRAN, class Hook>
 // (no __restrict__ here: with it the K/V and q loads may legally sink below the
 // hook's asm barrier once inlined; the standalone kernel keeps it on its arguments)
@@ -105,16 +195,18 @@ __device__ __forceinline__ bool attn_decode_body(bool active, int g, int s0, int
                                                  const uint16_t *vc, const StepState *step, int n_heads,
                                                  int n_kv_heads, int max_seq_len, int nsplit, unsigned long long *part,
                                                  unsigned ptag, unsigned *err, float *out, float *att_dbg,
-                                                 Hook &&hook, unsigned gtag = 0, int greps = 1) {
+                                                 Hook &&hook, unsigned gtag = 0, int greps = 1,
+                                                 unsigned long long *ts = nullptr, bool trace_on = false) {
 	constexpr int CHUNK = attn_chunk<D>();
-	constexpr int LPK = D / 8;                     // lanes per K/V row, 16 B each
-	constexpr int KPW = 64 / LPK;                  // rows per wave-instruction
-	constexpr int RSTEP = ATTN_WAVES * KPW;        // rows per workgroup-instruction
-	constexpr int NK = (CHUNK + RSTEP - 1) / RSTEP; // rows per lane
-	__shared__ __attribute__((aligned(16))) float sp[GT * CHUNK * LPK]; // per-lane partial dots
-	__shared__ float sc[GT][CHUNK];
-	__shared__ __attribute__((aligned(16))) float red[ATTN_WAVES * KPW][GT][D]; // per-row-slot P.V partials
-	__shared__ float ml[GT][2];
+	constexpr int LPK = D / 8;                      // lanes per K/V row, 16 B each
+	static_assert(LPK >= 2 && LPK <= 32 && (LPK & (LPK - 1)) == 0, "head_dim 16 .. 256, a power of two");
+	constexpr int KPW = 64 / LPK;                   // row groups per wave (rows per wave-instruction)
+	constexpr int RSTEP = ATTN_WAVES * KPW;         // rows per workgroup-instruction
+	constexpr int NK = CHUNK / RSTEP > 0 ? CHUNK / RSTEP : 1; // rows per lane (D 16: half the rows masked)
+	constexpr int QL = (GT * D + 255) / 256;        // 16-byte q loads per lane (wave-private copy)
+	__shared__ __attribute__((aligned(16))) float qs[ATTN_WAVES][GT * D];
+	__shared__ float wsum[ATTN_WAVES][GT][D]; // per-wave P.V sums
+	__shared__ float wml[ATTN_WAVES][GT][2];  // per-wave (max, sum of exp)
 
 	const int G = n_heads / n_kv_heads;
 	const int kv_dim = n_kv_heads * D;
@@ -134,23 +226,59 @@ __device__ __forceinline__ bool attn_decode_body(bool active, int g, int s0, int
 			vw[i] = load16(vc + off);
 		}
 	};
-	// ---- speculative loads of the first chunk (rows clamped to the cache), q and step in flight together
+	// ---- speculative loads: q of the group's G heads (G * D contiguous floats, QL
+	// 16-byte pieces per lane), the first chunk's K/V rows (clamped to the cache), step
+	const int gq = G * D;
+	float4_t qv[QL];
+#pragma unroll
+	for (int j = 0; j < QL; ++j)
+		qv[j] = *(const float4_t *)(q + (size_t)g * gq + min((j * 64 + lane) * 4, gq - 4));
 	u32x4_t kw[NK], vw[NK];
 	load_kv(s0 * CHUNK, kw, vw);
+	const int kv_len = step->kv_len; // issued before the hook's loads: its wait must not cover them
+	hook();
+	// trace (attn_wo.h, thread 0 only): s_memrealtime + shader clock (s_memtime) at
+	// checkpoint k, kept in registers and stored at the end -- a store issued mid-way
+	// would queue behind the co-resident Wo workgroup's weight loads and stall the wave
+	unsigned long long tsr[8] = {}, tsc[8] = {};
+	auto stamp = [&](int k) {
+		if (ts) {
+			tsr[k] = __builtin_amdgcn_s_memrealtime();
+			tsc[k] = __builtin_amdgcn_s_memtime();
+		}
+	};
+	auto flush = [&]() {
+		if (ts) {
+#pragma unroll
+			for (int k = 2; k < 8; ++k)
+				if (k != 3)
+					ts[k] = tsr[k], ts[8 + k] = tsc[k];
+		}
+	};
+	if (!active || s0 * CHUNK >= kv_len) {
+		flush();
+		return false; // whole workgroup leaves before any barrier
+	}
+	if (trace_on) { // tracing only: when the first chunk's loads have landed in every wave
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		__syncthreads();
+		stamp(2);
+	}
+	// q through this wave's own LDS copy: lane (row group, piece) needs dims piece*8..+8
+	// of every head (LDS reads from one wave are ordered after its writes: no barrier)
+#pragma unroll
+	for (int j = 0; j < QL; ++j)
+		if ((j * 64 + lane) * 4 < gq)
+			*(float4_t *)&qs[wave][(j * 64 + lane) * 4] = qv[j];
 	float qr[GT][8];
 #pragma unroll
 	for (int h = 0; h < GT; ++h) {
-		const int hh = h < G ? h : 0; // unconditional loads (no branch around each)
-		const float *qp = q + (size_t)(g * G + hh) * D + piece * 8;
+		const float *qp = &qs[wave][(h < G ? h : 0) * D + piece * 8];
 		const float4_t a = *(const float4_t *)qp;
 		const float4_t b = *(const float4_t *)(qp + 4);
 		qr[h][0] = a[0], qr[h][1] = a[1], qr[h][2] = a[2], qr[h][3] = a[3];
 		qr[h][4] = b[0], qr[h][5] = b[1], qr[h][6] = b[2], qr[h][7] = b[3];
 	}
-	const int kv_len = step->kv_len; // issued before the hook's loads: its wait must not cover them
-	hook();
-	if (!active || s0 * CHUNK >= kv_len)
-		return false; // whole workgroup leaves before any barrier
 	const int ns = (kv_len + CHUNK - 1) / CHUNK;
 	const float sq = sqrtf((float)D);
 
@@ -160,139 +288,233 @@ __device__ __forceinline__ bool attn_decode_body(bool active, int g, int s0, int
 		if (cidx != s0)
 			load_kv(t0, kw, vw);
 		const int nt = min(CHUNK, kv_len - t0);
+		float acc[GT * 8]; // this lane's P.V sums: element e of head h at dim piece * 8 + e
+#pragma unroll
+		for (int k = 0; k < GT * 8; ++k)
+			acc[k] = 0.0f;
 
-		// ---- scores: each lane's 8-element partial dots go to LDS; one thread per
-		// (head, key) then sums the D/8 partials in piece order (no shuffles)
+		if constexpr (LPK == 16) {
+			// ---- head_dim 128: the row's 16 lanes share out its NK * GT scores (V values,
+			// padded to 16 J): a 4-step reduce-scatter of the partial dots leaves lane p of
+			// the row with score f = 16 j + p (key row i = f / GT, head h = f % GT), so
+			// the exp, max and sum run once per score, not once per lane
+			constexpr int V = NK * GT, J = V >= 16 ? V / 16 : 1;
+			float d16[J * 16];
+			{
+				float kf[NK][8];
 #pragma unroll
-		for (int i = 0; i < NK; ++i) {
-			const int tl = tl0 + i * RSTEP;
-			float kf[8];
-			WF16::unpack(kw[i], kf);
+				for (int i = 0; i < NK; ++i)
+					WF16::unpack(kw[i], kf[i]);
 #pragma unroll
-			for (int h = 0; h < GT; ++h) {
-				float d = 0.0f;
+				for (int f = 0; f < J * 16; ++f) {
+					float d = 0.0f;
+					if (f < V) {
 #pragma unroll
-				for (int e = 0; e < 8; ++e)
-					d = fmaf(qr[h][e], kf[e], d);
-				if (h < G && tl < CHUNK)
-					sp[(h * CHUNK + tl) * LPK + piece] = d;
-			}
-		}
-		__syncthreads();
-		for (int i = tid; i < G * CHUNK; i += ATTN_THREADS) {
-			const int h = i / CHUNK, t = i % CHUNK;
-			const float *pp = &sp[(h * CHUNK + t) * LPK];
-			float d = 0.0f;
-			if constexpr (LPK >= 4) {
-#pragma unroll
-				for (int j = 0; j < LPK; j += 4) {
-					const float4_t v = *(const float4_t *)(pp + j);
-					d += v[0] + v[1] + v[2] + v[3];
+						for (int e = 0; e < 8; ++e)
+							d = fmaf(qr[f % GT][e], kf[f / GT][e], d);
+					}
+					d16[f] = d;
 				}
-			} else {
-#pragma unroll
-				for (int j = 0; j < LPK; ++j)
-					d += pp[j];
 			}
-			sc[h][t] = d / sq;
-		}
-		__syncthreads();
-
-		// ---- chunk-local softmax statistics; wave w owns heads w, w+4, ... (DPP reductions)
-		for (int h = wave; h < G; h += ATTN_WAVES) {
+			float r8[J * 8], r4[J * 4], r2[J * 2], sc[J];
+			attn_rs_step<0x140, J, 16>(d16, r8, lane & 8); // row_mirror: lanes p, 15 - p
+			attn_rs_step<0x141, J, 8>(r8, r4, lane & 4);   // row_half_mirror: p, p ^ 7
+			attn_rs_step<0x4E, J, 4>(r4, r2, lane & 2);    // quad_perm xor 2
+			attn_rs_step<0xB1, J, 2>(r2, sc, lane & 1);    // quad_perm xor 1
+			const int p = lane & 15, h = p % GT;
+			bool ok[J];
 			float m = -FLT_MAX;
-			for (int t = lane; t < nt; t += 64)
-				m = fmaxf(m, sc[h][t]);
-			m = wave_max(m);
-			float l = 0.0f;
-			for (int t = lane; t < nt; t += 64) {
-				const float sv = sc[h][t];
-				if (att_dbg)
-					st_sc1(att_dbg + (size_t)(g * G + h) * max_seq_len + t0 + t, sv);
-				const float p = expf(sv - m);
-				sc[h][t] = p;
-				l += p;
+#pragma unroll
+			for (int j = 0; j < J; ++j) {
+				const int f = j * 16 + p, i = f / GT;
+				ok[j] = f < V && tl0 + i * RSTEP < nt;
+				sc[j] = sc[j] / sq;
+				m = ok[j] ? fmaxf(m, sc[j]) : m;
+				if (att_dbg && ok[j] && h < G) // test hook: raw scores (normalised after the barrier)
+					st_sc1(att_dbg + (size_t)(g * G + h) * max_seq_len + t0 + tl0 + i * RSTEP, sc[j]);
 			}
-			l = wave_sum(l);
-			if (lane == 0) {
-				ml[h][0] = m;
-				ml[h][1] = l;
+			stamp(4);
+			// ---- per-wave softmax statistics of head h: over the row's lanes of the same
+			// head (row_ror by GT, 2 GT, ..), then over the 4 rows
+			m = attn_wave_red<GT, true>(m);
+			float pj[J], l = 0.0f;
+#pragma unroll
+			for (int j = 0; j < J; ++j) {
+				pj[j] = ok[j] ? expf(sc[j] - m) : 0.0f;
+				l += pj[j];
 			}
-		}
-		__syncthreads();
-
-		// ---- P.V from the loaded V rows; per-row-slot partials to LDS
-		float acc[GT][8];
-#pragma unroll
-		for (int h = 0; h < GT; ++h)
-#pragma unroll
-			for (int e = 0; e < 8; ++e)
-				acc[h][e] = 0.0f;
-#pragma unroll
-		for (int i = 0; i < NK; ++i) {
-			const int tl = tl0 + i * RSTEP;
-			const float pv = tl < nt ? 1.0f : 0.0f;
-			float vf[8];
-			WF16::unpack(vw[i], vf);
-#pragma unroll
-			for (int h = 0; h < GT; ++h) {
-				const float p = tl < nt ? sc[h < G ? h : 0][tl < CHUNK ? tl : 0] : 0.0f;
-#pragma unroll
-				for (int e = 0; e < 8; ++e)
-					acc[h][e] = fmaf(p, vf[e] * pv, acc[h][e]);
+			l = attn_wave_red<GT, false>(l);
+			if (lane < GT && lane < G) {
+				wml[wave][lane][0] = m;
+				wml[wave][lane][1] = l;
 			}
-		}
-		{
-			const int slot = wave * KPW + sub;
+			stamp(5);
+			// ---- P.V: probability f is broadcast from lane f % 16 of each row (row_newbcast)
 #pragma unroll
-			for (int h = 0; h < GT; ++h) {
-				if (h < G) {
-					float *rp = &red[slot][h][piece * 8];
-					*(float4_t *)rp = float4_t{acc[h][0], acc[h][1], acc[h][2], acc[h][3]};
-					*(float4_t *)(rp + 4) = float4_t{acc[h][4], acc[h][5], acc[h][6], acc[h][7]};
+			for (int i = 0; i < NK; ++i) {
+				float vf[8];
+				const bool valid = tl0 + i * RSTEP < nt;
+				WF16::unpack(valid ? vw[i] : u32x4_t{0u, 0u, 0u, 0u}, vf); // rows past kv_len may hold anything
+#pragma unroll
+				for (int hh = 0; hh < GT; ++hh) {
+					const int f = i * GT + hh;
+					const float pv = row_bcast16(pj[f / 16], f % 16);
+#pragma unroll
+					for (int e = 0; e < 8; ++e)
+						acc[hh * 8 + e] = fmaf(pv, vf[e], acc[hh * 8 + e]);
 				}
 			}
-		}
-		__syncthreads();
-
-		if (ns == 1) { // single chunk: normalise and write the head outputs directly
-			for (int i = tid; i < G * D; i += ATTN_THREADS) {
-				const int h = i / D, d = i % D;
-				float o = 0.0f;
+		} else {
+			// ---- other head dims: every lane of a row group reduces all its rows' scores
+			float sv[NK][GT];
+			bool valid[NK];
 #pragma unroll
-				for (int w = 0; w < ATTN_WAVES * KPW; ++w)
-					o += red[w][h][d];
-				attn_out_rep<GRAN>(out, (size_t)(g * G + h) * D + d, o / ml[h][1], gtag, greps, (size_t)n_heads * D);
-			}
-			if (att_dbg) {
-				for (int i = tid; i < G * nt; i += ATTN_THREADS) {
-					const int h = i / nt, t = i % nt;
-					att_dbg[(size_t)(g * G + h) * max_seq_len + t] = sc[h][t] / ml[h][1];
+			for (int i = 0; i < NK; ++i) {
+				valid[i] = tl0 + i * RSTEP < nt;
+				float kf[8];
+				WF16::unpack(kw[i], kf);
+#pragma unroll
+				for (int h = 0; h < GT; ++h) {
+					float d = 0.0f;
+#pragma unroll
+					for (int e = 0; e < 8; ++e)
+						d = fmaf(qr[h][e], kf[e], d);
+					sv[i][h] = attn_row_sum<LPK>(d) / sq;
 				}
 			}
-			return true;
+			if (att_dbg && piece == 0) { // test hook: raw scores (normalised after the barrier)
+#pragma unroll
+				for (int i = 0; i < NK; ++i)
+#pragma unroll
+					for (int h = 0; h < GT; ++h)
+						if (valid[i] && h < G)
+							st_sc1(att_dbg + (size_t)(g * G + h) * max_seq_len + t0 + tl0 + i * RSTEP, sv[i][h]);
+			}
+			stamp(4);
+			float mw[GT], lw[GT];
+#pragma unroll
+			for (int h = 0; h < GT; ++h) {
+				float m = -FLT_MAX;
+#pragma unroll
+				for (int i = 0; i < NK; ++i)
+					m = valid[i] ? fmaxf(m, sv[i][h]) : m;
+				m = attn_wave_red<LPK, true>(m);
+				float l = 0.0f;
+#pragma unroll
+				for (int i = 0; i < NK; ++i) {
+					sv[i][h] = valid[i] ? expf(sv[i][h] - m) : 0.0f;
+					l += sv[i][h];
+				}
+				mw[h] = m;
+				lw[h] = attn_wave_red<LPK, false>(l);
+			}
+			if (lane < GT && lane < G) {
+				float m = mw[0], l = lw[0];
+#pragma unroll
+				for (int h = 1; h < GT; ++h)
+					if (lane == h)
+						m = mw[h], l = lw[h];
+				wml[wave][lane][0] = m;
+				wml[wave][lane][1] = l;
+			}
+			stamp(5);
+#pragma unroll
+			for (int i = 0; i < NK; ++i) {
+				float vf[8];
+				WF16::unpack(valid[i] ? vw[i] : u32x4_t{0u, 0u, 0u, 0u}, vf); // rows past kv_len may hold anything
+#pragma unroll
+				for (int h = 0; h < GT; ++h)
+#pragma unroll
+					for (int e = 0; e < 8; ++e)
+						acc[h * 8 + e] = fmaf(sv[i][h], vf[e], acc[h * 8 + e]);
+			}
 		}
 
-		// ---- publish this chunk's partial (o[D], m, l per head) as tagged granules
-		if (att_dbg) // test hook: the raw scores must be visible before the merger sees the tags
+		// ---- this wave's P.V sums over its row groups, into LDS
+		if constexpr (LPK <= 16) {
+			// the row groups inside each DPP row first (LPK < 16), then across the 4 DPP
+			// rows transposed: for value group k, lane `piece` of DPP row r holds value
+			// 4k + r of that piece summed over the wave (element e of head h: dim piece * 8 + e)
+#pragma unroll
+			for (int k = 0; k < GT * 8; ++k)
+				acc[k] = attn_fold_row<LPK, false>(acc[k]);
+#pragma unroll
+			for (int k = 0; k < GT * 2; ++k) {
+				const float v4[4] = {acc[4 * k], acc[4 * k + 1], acc[4 * k + 2], acc[4 * k + 3]};
+				const float s = sum4_rows(v4);
+				const int idx = 4 * k + (lane >> 4), h = idx >> 3, e = idx & 7;
+				if (h < G && (lane & 15) < LPK)
+					wsum[wave][h][(lane & 15) * 8 + e] = s;
+			}
+		} else { // LPK 32: two row groups, the wave's halves
+#pragma unroll
+			for (int k = 0; k < GT * 8; ++k)
+				acc[k] += xor32(acc[k]);
+			if (lane < 32) {
+#pragma unroll
+				for (int h = 0; h < GT; ++h)
+#pragma unroll
+					for (int e = 0; e < 8; ++e)
+						if (h < G)
+							wsum[wave][h][lane * 8 + e] = acc[h * 8 + e];
+			}
+		}
+		if (att_dbg) // test hook: every wave's raw scores visible before the barrier
 			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		__syncthreads();
+		stamp(6);
+
+		// ---- combine the waves (fixed order): o = sum_w e^(m_w - M) o_w, L likewise
 		for (int i = tid; i < G * D; i += ATTN_THREADS) {
 			const int h = i / D, d = i % D;
-			float o = 0.0f;
+			float M = wml[0][h][0];
 #pragma unroll
-			for (int w = 0; w < ATTN_WAVES * KPW; ++w)
-				o += red[w][h][d];
-			attn_out<true>((float *)part, ((size_t)(g * G + h) * nsplit + cidx) * (D + 2) + d, o, ptag);
+			for (int w = 1; w < ATTN_WAVES; ++w)
+				M = fmaxf(M, wml[w][h][0]);
+			float o = 0.0f, L = 0.0f;
+#pragma unroll
+			for (int w = 0; w < ATTN_WAVES; ++w) {
+				const float c = expf(wml[w][h][0] - M); // 0 for a wave without valid rows (m_w = -FLT_MAX)
+				o = fmaf(wsum[w][h][d], c, o);
+				L = fmaf(wml[w][h][1], c, L);
+			}
+			if (ns == 1) { // single chunk: normalise and write the head outputs directly
+				attn_out_rep<GRAN>(out, (size_t)(g * G + h) * D + d, o / L, gtag, greps, (size_t)n_heads * D);
+			} else { // this chunk's partial (o[D], M, L per head) as tagged granules
+				const size_t pp = ((size_t)(g * G + h) * nsplit + cidx) * (D + 2);
+				attn_out<true>((float *)part, pp + d, o, ptag);
+				if (d == 0) {
+					attn_out<true>((float *)part, pp + D, M, ptag);
+					attn_out<true>((float *)part, pp + D + 1, L, ptag);
+				}
+			}
 		}
-		if (tid < G) {
-			const size_t pp = ((size_t)(g * G + tid) * nsplit + cidx) * (D + 2);
-			attn_out<true>((float *)part, pp + D, ml[tid][0], ptag);
-			attn_out<true>((float *)part, pp + D + 1, ml[tid][1], ptag);
+		if (ns == 1) {
+			if (att_dbg) { // test hook: raw scores -> probabilities
+				for (int i = tid; i < G * nt; i += ATTN_THREADS) {
+					const int h = i / nt, t = i % nt;
+					float M = wml[0][h][0];
+#pragma unroll
+					for (int w = 1; w < ATTN_WAVES; ++w)
+						M = fmaxf(M, wml[w][h][0]);
+					float L = 0.0f;
+#pragma unroll
+					for (int w = 0; w < ATTN_WAVES; ++w)
+						L = fmaf(wml[w][h][1], expf(wml[w][h][0] - M), L);
+					float *a = att_dbg + (size_t)(g * G + h) * max_seq_len + t;
+					*a = expf(ld_sc1(a) - M) / L;
+				}
+			}
+			flush();
+			return true;
 		}
-		__syncthreads(); // LDS (sp, sc, ml, red) reused by the next chunk
+		if (cidx + S < ns)
+			__syncthreads(); // wsum / wml are rewritten by the next chunk
 	}
-	if (s0 != min(ns, S) - 1)
+	if (s0 != min(ns, S) - 1) {
+		flush();
 		return false; // not the merger: nothing to wait for
+	}
 
 	// ---- merger: gather the ns chunk partials of heads g*G .. as granules, re-reading
 	// a batch of MB chunks until every tag holds ptag (one round trip when the other
@@ -367,6 +589,7 @@ __device__ __forceinline__ bool attn_decode_body(bool active, int g, int s0, int
 			}
 			M = Mn;
 		}
+		stamp(7);
 		if (lane < D) {
 #pragma unroll
 			for (int k = 0; k < DPL; ++k)
@@ -380,6 +603,7 @@ __device__ __forceinline__ bool attn_decode_body(bool active, int g, int s0, int
 			}
 		}
 	}
+	flush();
 	return true;
 }
 

@@ -43,6 +43,7 @@
 #define AWO_TIMEOUT 200000000ull     // 2 s of s_memrealtime (100 MHz)
 #define AWO_REPL_STRIDE 32           // words of the error slot (a 128-B line of its own)
 #define AWO_GR 8                     // max copies of the head outputs per layer (one per XCD)
+#define AWO_TRACE_N 16               // s_memrealtime + s_memtime stamps per workgroup (yalm_attn_wo_trace)
 
 struct AttnWoArgs {
 	int n_heads, n_kv, max_seq_len, nsplit, S; // S = key-chunk splits per kv head: n_kv * S attention workgroups
@@ -53,7 +54,7 @@ struct AttnWoArgs {
 	const char *wo;     // Wo (dim, q_dim)
 	float *x;           // residual stream (dim)
 	unsigned *err;      // error bits (bounded spin gave up)
-	unsigned long long *trace; // [grid][4] s_memrealtime stamps (YALM_ATTN_WO_TRACE=1) or null
+	unsigned long long *trace; // [grid][AWO_TRACE_N] s_memrealtime stamps (YALM_ATTN_WO_TRACE=1) or null
 	int win;            // Wo loads in flight per lane: 0 = all at once, 8 / 16 / 24 (YALM_ATTN_WO_WIN);
 	                    // -1 = no weight loads (YALM_ABLATE bit 32, timing only: results wrong)
 	int delay;          // s_memrealtime ticks (10 ns) the Wo workgroups wait before their slice loads
@@ -225,19 +226,24 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 	static_assert(ATTN_THREADS == 256 && ATTN_WAVES == 4, "4-wave workgroups: one 4-row reduction per wave");
 	const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 	const int units = p.n_kv * p.S;
-	unsigned long long *tr = p.trace && tid == 0 ? p.trace + (size_t)b * 4 : nullptr;
-	if (tr) // [0] start, [1] hand-off signalled / Wo slice landed, [2] poll passed, [3] end
-		tr[0] = __builtin_amdgcn_s_memrealtime(), tr[1] = tr[2] = tr[3] = 0;
+	// include/yalm_hip.h yalm_attn_wo_trace: [0] start, [1] hand-off signalled / Wo slice landed, ...
+	// (kept in registers, stored when the workgroup is done: see attention.h `stamp`)
+	unsigned long long *tr = p.trace && tid == 0 ? p.trace + (size_t)b * AWO_TRACE_N : nullptr;
+	unsigned long long t_start = 0, c_start = 0;
+	if (tr)
+		t_start = __builtin_amdgcn_s_memrealtime(), c_start = __builtin_amdgcn_s_memtime();
 
 	const unsigned epoch = step->epoch; // this launch's tag (step_begin_kernel / set_step_full_kernel)
 	if (b < units) { // ---- attention workgroup
 		const bool wrote = attn_decode_body<D, GT, true>(
 		    true, b % p.n_kv, b / p.n_kv, p.S, q, kc, vc, step, p.n_heads, p.n_kv, p.max_seq_len, p.nsplit, p.part,
-		    epoch * (unsigned)p.n_layers + (unsigned)p.layer, p.err, (float *)p.gran, nullptr, [] {}, epoch, p.greps);
-		if (wrote && tr) // the head outputs are their own ready flags: nothing to drain or signal
-			tr[1] = __builtin_amdgcn_s_memrealtime();
-		if (tr)
-			tr[3] = __builtin_amdgcn_s_memrealtime();
+		    epoch * (unsigned)p.n_layers + (unsigned)p.layer, p.err, (float *)p.gran, nullptr, [] {}, epoch, p.greps, tr, p.trace != nullptr);
+		if (tr) { // the head outputs are their own ready flags: nothing to drain or signal
+			const unsigned long long t1 = __builtin_amdgcn_s_memrealtime(), c1 = __builtin_amdgcn_s_memtime();
+			tr[0] = t_start, tr[8] = c_start;
+			tr[1] = wrote ? t1 : 0, tr[9] = wrote ? c1 : 0;
+			tr[3] = t1, tr[11] = c1;
+		}
 		return;
 	}
 
@@ -269,9 +275,10 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 		}
 		wr[i] = p.win >= 0 ? load_nt16(wbase + ((size_t)i * ATTN_THREADS + tid) * 16) : u32x4_t{0u, 0u, 0u, 0u};
 	}
+	unsigned long long t_slice = 0, c_slice = 0, t_poll = 0, c_poll = 0;
 	if (tr) { // tracing only: when the whole slice has landed
 		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-		tr[1] = __builtin_amdgcn_s_memrealtime();
+		t_slice = __builtin_amdgcn_s_memrealtime(), c_slice = __builtin_amdgcn_s_memtime();
 	}
 
 	// ---- per wave: gather this lane's input columns as {value, tag} granules with
@@ -283,7 +290,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 	if (!awo_gather_gran<EPL, XS>(xs, gran, tid, epoch, t0 + AWO_TIMEOUT, p.spec != 0) && lane == 0)
 		__hip_atomic_fetch_or(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 	if (tr)
-		tr[2] = __builtin_amdgcn_s_memrealtime();
+		t_poll = __builtin_amdgcn_s_memrealtime(), c_poll = __builtin_amdgcn_s_memtime();
 	float a0[AWO_RPW], a1[AWO_RPW];
 #pragma unroll
 	for (int r = 0; r < AWO_RPW; ++r) {
@@ -309,7 +316,11 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 		const float s = (rowpart[tid][0] + rowpart[tid][1]) + (rowpart[tid][2] + rowpart[tid][3]);
 		p.x[row] += s;
 	}
-	if (tr)
-		tr[3] = __builtin_amdgcn_s_memrealtime();
+	if (tr) {
+		tr[3] = __builtin_amdgcn_s_memrealtime(), tr[11] = __builtin_amdgcn_s_memtime();
+		tr[0] = t_start, tr[8] = c_start, tr[1] = t_slice, tr[9] = c_slice, tr[2] = t_poll, tr[10] = c_poll;
+		for (int k = 4; k < 8; ++k)
+			tr[k] = tr[8 + k] = 0;
+	}
 }
 

@@ -191,15 +191,20 @@ __device__ __forceinline__ void dot16_mix(float &a0, float &a1, const u32x4_t &w
 	}
 }
 
-// Sums of 4 per-lane values over the wave, transposed: lanes 16 t .. 16 t + 15 end
-// with the total of v[t]. Each exchange sends the value the partner keeps and keeps
-// the one it sends back (2 xor-32 + 1 xor-16 lane swaps), then one 16-lane DPP sum.
-__device__ __forceinline__ float sum4_t(const float (&v)[4]) {
+// Sums of 4 per-lane values over the wave's 4 rows (16-lane groups), transposed:
+// lane p of row r ends with v[r] summed over lane p of all 4 rows. Each exchange
+// sends the value the partner keeps and keeps the one it sends back (2 xor-32 +
+// 1 xor-16 lane swaps instead of 4 x 2).
+__device__ __forceinline__ float sum4_rows(const float (&v)[4]) {
 	const bool hi32 = threadIdx.x & 32, odd16 = threadIdx.x & 16;
-	const float s02 = (hi32 ? v[2] : v[0]) + xor32(hi32 ? v[0] : v[2]); // lanes 0-31: row 0, 32-63: row 2
-	const float s13 = (hi32 ? v[3] : v[1]) + xor32(hi32 ? v[1] : v[3]); // row 1 / row 3
-	const float u = (odd16 ? s13 : s02) + xor16(odd16 ? s02 : s13);     // 16-lane group g: row g
-	return row16_sum(u);
+	const float s02 = (hi32 ? v[2] : v[0]) + xor32(hi32 ? v[0] : v[2]); // lanes 0-31: v[0], 32-63: v[2]
+	const float s13 = (hi32 ? v[3] : v[1]) + xor32(hi32 ? v[1] : v[3]); // v[1] / v[3]
+	return (odd16 ? s13 : s02) + xor16(odd16 ? s02 : s13);              // row r: v[r]
+}
+// Sums of 4 per-lane values over the whole wave, transposed: lanes 16 t .. 16 t + 15
+// end with the total of v[t].
+__device__ __forceinline__ float sum4_t(const float (&v)[4]) {
+	return row16_sum(sum4_rows(v));
 }
 
 // infer.cu:586-596 semantics (SiLU x/(1+e^-x); GELU tanh approximation).

@@ -361,7 +361,7 @@ static int attn_wo_init(yalm_decoder_s *d) {
 	d->awo_greps = renv ? std::max(1, std::min(AWO_GR, atoi(renv))) : 1;
 	const char *tenv = getenv("YALM_ATTN_WO_TRACE");
 	if (tenv && atoi(tenv) != 0)
-		TRY(dalloc(d, (void **)&d->awo_trace, sizeof(unsigned long long) * 4 * d->awo_nb));
+		TRY(dalloc(d, (void **)&d->awo_trace, sizeof(unsigned long long) * AWO_TRACE_N * d->awo_nb));
 	d->attn_wo = true;
 	return YALM_OK;
 }
@@ -1148,7 +1148,7 @@ extern "C" int yalm_attn_wo_trace(yalm_decoder d, unsigned long long *host, size
 	ARGCHK(d && host, "null argument");
 	ARGCHK(d->attn_wo && d->awo_trace, "no attn_wo trace (create the decoder with YALM_ATTN_WO_TRACE=1)");
 	HIPCHK(hipStreamSynchronize(d->stream));
-	const size_t total = (size_t)4 * d->awo_nb;
+	const size_t total = (size_t)AWO_TRACE_N * d->awo_nb;
 	HIPCHK(hipMemcpy(host, d->awo_trace, sizeof(unsigned long long) * std::min(count, total), hipMemcpyDeviceToHost));
 	if (workgroups)
 		*workgroups = d->awo_nb;

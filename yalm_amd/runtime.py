@@ -17,7 +17,8 @@ import numpy as np
 from . import models as M
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libyalm_hip.so")
+# YALM_LIB: another build of the same ABI (A/B timing of two revisions, tools/build_ab_lib.sh)
+LIB_PATH = os.environ.get("YALM_LIB") or os.path.join(HERE, "libyalm_hip.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(
@@ -450,12 +451,12 @@ class Decoder:
         return bool(lib.yalm_decoder_attn_wo(self.h))
 
     def attn_wo_trace(self):
-        """((workgroups, 4) uint64 stamps, attention workgroups) of the last fused
+        """((workgroups, 16) uint64 stamps, attention workgroups) of the last fused
         attention + Wo launch (decoder created with YALM_ATTN_WO_TRACE=1)."""
-        buf = np.zeros(4 * 8192, np.uint64)
+        buf = np.zeros(16 * 8192, np.uint64)
         nb, na = c_int(), c_int()
         check(lib.yalm_attn_wo_trace(self.h, buf.ctypes.data, buf.size, ctypes.byref(nb), ctypes.byref(na)))
-        return buf[: 4 * nb.value].reshape(nb.value, 4), na.value
+        return buf[: 16 * nb.value].reshape(nb.value, 16), na.value
 
     def kernel_name(self, kernel_id: int) -> str:
         return lib.yalm_kernel_name(self.h, kernel_id).decode()
