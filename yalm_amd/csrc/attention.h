@@ -179,14 +179,14 @@ __device__ __forceinline__ float attn_wave_red(float v) {
 // set if the merger's bounded wait gave up (results wrong, reported).
 // ts / trace_on: attn_wo.h's timeline stamps (thread 0) and the trace-only waits.
 //
-// Round 4 layout: each wave runs its 16 keys of the chunk to the end WITHOUT a
+// Layout: each wave runs its 16 keys of the chunk to the end WITHOUT a
 // workgroup barrier -- lane (row group, piece) holds 8 dims of NK K/V rows; the
 // scores are reduced across the row's pieces with DPP, the softmax statistics
 // are per wave (max / sum across row groups with DPP and lane swaps), P is never
 // stored, and the P.V sums are reduced across row groups in registers (transposed
 // sum4_rows). One barrier per chunk then combines the 4 waves' (m, l, o) with
-// the flash-decoding rescaling. Round 3 staged the partial dots, the scores and
-// the P.V partials through LDS behind 4 barriers (~6700 shader clocks from the
+// the flash-decoding rescaling. Before commit 59434d2 the partial dots, the scores and
+// the P.V partials went through LDS behind 4 barriers (~6700 shader clocks from the
 // loads landing to the head outputs; tools/attn_wo_trace.py).
 template <int D, int GT, bool GRAN, class Hook>
 // (no __restrict__ here: with it the K/V and q loads may legally sink below the

@@ -344,10 +344,12 @@ static int attn_wo_init(yalm_decoder_s *d) {
 	}
 	d->awo_win = d->ablate & 32 ? -1 : win; // ablation bit 32: no Wo weight loads (timing only)
 	const char *denv = getenv("YALM_ATTN_WO_DELAY");
-	// default 0.2 us: the attention workgroups' K/V loads reach HBM ahead of the 33.5 MB Wo
-	// stream (tools/sweep_awo.sh, profiles/r2_sweep_awo_delay.txt: 10.6 -> 10.1 us at kv_len 17,
-	// 10.6 -> 10.4 at kv_len 151; 0.4-0.6 us delays lose it again at long contexts)
-	d->awo_delay = denv ? std::max(0, atoi(denv)) : 20;
+	// default 0.2 us (fp16) / 0.5 us (fp8): the attention workgroups' K/V loads reach HBM
+	// ahead of the Wo stream. fp16 (33.5 MB, slice lands ~5.4 us, after the heads):
+	// profiles/r2_sweep_awo_delay.txt 10.6 -> 10.1 us at kv_len 17. fp8 (16.8 MB, slice lands
+	// ~3.1 us, before the heads): 0.5 us gives 9.4 -> 8.4 us at kv 17, 11.3 -> 10.3 at kv 151,
+	// 579 -> 586 tok/s (profiles/r3_ab_awo_delay.txt); fp16 at 0.5 us is within noise
+	d->awo_delay = denv ? std::max(0, atoi(denv)) : (c.weight_dtype == YALM_F8E5M2 ? 50 : 20);
 	// combined first attempt (gather + sentinels in one round trip once the slice has
 	// landed, attn_wo.h awo_gather_gran): opt-in, YALM_AWO_SPEC=1. Measured with a fresh
 	// epoch per timed launch it loses (profiles/r3_ab_awo.txt): fp8 kv 17
