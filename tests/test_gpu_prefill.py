@@ -43,20 +43,24 @@ def test_gemm_exact_integers(M_, N, K):
 # 128 x 256 ("wide") tile; read per launch from the environment
 # (the 128-tile forms switch the large-tile kernel off: YALM_PF_G16=0); "g16-256" /
 # "g16-128": prefill_gemm.h gemm16_kernel with 256 x 256 / 256 x 128 tiles everywhere
+# ("g16-256" runs the 8-phase gemm8p_kernel, "g16-256-2ph" the 2-phase gemm16_kernel)
 G16_ALL = "qkv:{0},wo:{0},glu:{0},w2:{0},cls:{0},test:{0}"
 FORMS = {"auto": {}, "s2": {"YALM_PF_STAGES": "2", "YALM_PF_G16": "0"}, "s3": {"YALM_PF_STAGES": "3", "YALM_PF_G16": "0"},
          "s3-wide": {"YALM_PF_STAGES": "3", "YALM_PF_WIDE": "1", "YALM_PF_G16": "0"},
          "s2-wide": {"YALM_PF_STAGES": "2", "YALM_PF_WIDE": "1", "YALM_PF_G16": "0"},
          "s3-narrow": {"YALM_PF_STAGES": "3", "YALM_PF_WIDE": "0", "YALM_PF_G16": "0"},
-         "g16-256": {"YALM_PF_G16": G16_ALL.format(256)}, "g16-128": {"YALM_PF_G16": G16_ALL.format(128)},
+         "g16-256": {"YALM_PF_G16": G16_ALL.format(256)},
+         "g16-256-2ph": {"YALM_PF_G16": G16_ALL.format(256), "YALM_PF_8P": "0"}, "g16-128": {"YALM_PF_G16": G16_ALL.format(128)},
          "g16-192": {"YALM_PF_G16": G16_ALL.format(192)}, "g16-320": {"YALM_PF_G16": G16_ALL.format(320)}}
 
 
 @pytest.mark.parametrize("form", list(FORMS))
-@pytest.mark.parametrize("M_,N,K", [(200, 256, 192), (37, 768, 128), (1, 256, 64), (513, 5120, 640), (300, 384, 64)])
+@pytest.mark.parametrize("M_,N,K", [(200, 256, 192), (37, 768, 128), (1, 256, 64), (513, 5120, 640), (300, 384, 64),
+                                    (513, 512, 320), (260, 768, 448), (256, 256, 576), (70, 512, 128)])
 def test_gemm_forms_exact(form, M_, N, K, monkeypatch):
     """Every stage count / tile form is exact on f16-exact integer data (any
-    staging race or fragment-map error shows as a wrong integer); K tiles 1..10."""
+    staging race or fragment-map error shows as a wrong integer); K tiles 1..10
+    (odd and even counts: the 8-phase kernel's iteration covers two K tiles)."""
     for k, v in FORMS[form].items():
         monkeypatch.setenv(k, v)
     rng = np.random.default_rng(M_ + N + K)
@@ -127,7 +131,7 @@ CFGS = {
 
 
 @pytest.mark.parametrize("cfg_name", ["gqa-d128", "d768"])
-@pytest.mark.parametrize("form", ["auto", "s3", "s2-wide", "g16-256", "g16-128", "g16-192", "g16-320"])
+@pytest.mark.parametrize("form", ["auto", "s3", "s2-wide", "g16-256", "g16-256-2ph", "g16-128", "g16-192", "g16-320"])
 def test_prefill_forms_match_decode(form, cfg_name, monkeypatch):
     """The whole prefill in each GEMM form (the wide tile on every GEMM with N %
     256 == 0, incl. the vocab-tiled logits epilogue run once per column half)."""

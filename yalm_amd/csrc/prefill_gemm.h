@@ -353,4 +353,187 @@ constexpr size_t gemm16_lds() {
 	return (size_t)2 * (G_BM + BN) * G_BK * sizeof(uint16_t);
 }
 
+// ---------------------------------------------------------------- 8-phase 256 x 256 GEMM
+// The same C = A · B^T tile as gemm16_kernel<BN 256, WM 2> (8 waves as 2 M x 4 N, each
+// wave 128 x 64 outputs, v_mfma_f32_16x16x32_f16), with the K loop cut into PHASES
+// (cdna_hip_programming.md §5 "The 256² 8-phase template", T3+T4) instead of one
+// stage / read / MFMA / drain / barrier step per K tile:
+//
+// * LDS: 2 buffers (E, O) x 4 HALF-TILES of 128 rows x 64 k (16 KB each) = 128 KB:
+//     Am0 = the first 64 rows of each wave row's 128 (tile rows 0-63, 128-191),
+//     Am1 = the other 64 (64-127, 192-255),
+//     Bn0 = the first 32 B rows of each wave column's 64 (0-31, 64-95, 128-159, 192-223),
+//     Bn1 = the other 32.
+// * A K tile is 4 phases, one output quadrant each (16 MFMAs per wave):
+//     q1 (m0, n0): read Am0 -> a, Bn0 -> b0     q2 (m0, n1): read Bn1 -> b1
+//     q3 (m1, n1): read Am1 -> a                q4 (m1, n0): no read (a, b0 held)
+//   so a half-tile's last LDS read in a K tile is q1 (Am0, Bn0), q2 (Bn1) or q3 (Am1).
+// * Every phase stages ONE half-tile (2 LDS-DMAs per thread) and waits vmcnt(8): the
+//   half-tile issued 4 phases earlier has landed, 4 stay in flight across the barriers
+//   (no vmcnt(0) in the loop). Iteration = 8 phases = K tiles 2i (E) and 2i + 1 (O);
+//   stage order: p1 Bn1 O(2i+1), p2 Am1 O(2i+1), p3 Am0 E(2i+2), p4 Bn0 E(2i+2),
+//   p5 Bn1 E(2i+2), p6 Am1 E(2i+2), p7 Am0 O(2i+3), p8 Bn0 O(2i+3).
+// * The two wave rows run one barrier apart (wave row 1 passes one extra barrier
+//   first): each phase is {reads, stage, vmcnt} barrier {MFMAs} barrier, so on every
+//   SIMD one wave's MFMAs run while the other's LDS reads and DMA issue do.
+// * Hazards, with barrier intervals I_k (between barriers k and k + 1 of an iteration;
+//   wave row 0 reads / stages phase p in I_{2p-2}, row 1 in I_{2p-1}; a ds_read issued
+//   in I_k is complete before its wave reaches barrier k + 2):
+//     WAR: a half-tile is restaged at phase s only when its last reader's interval is
+//       <= 2s - 4 (Am0/Bn0 of E read last in I_1, restaged from I_4; Bn1 I_3 -> I_8;
+//       Am1 I_5 -> I_10; O: I_9 -> I_12 / I_14, I_11 -> I_16, I_13 -> I_18).
+//     RAW: the half-tile staged at phase s is retired by both rows' vmcnt(8) at phase
+//       s + 4 (row 1: before barrier 2s + 8) and first read at phase >= s + 5 (row 0:
+//       after barrier 2s + 8).
+// * Tail: phases whose K tile is past the end stage nothing and wait vmcnt(0).
+constexpr int P8_HT = 128 * G_BK; // f16 per half-tile
+
+template <class EPI, class BMAP>
+__global__ __launch_bounds__(G_THREADS, 1) void gemm8p_kernel(const uint16_t *__restrict__ A, int M, int K, BMAP bm,
+                                                             int N, EPI epi) {
+	constexpr int BN = 256, TM = 128, TN = 64, FI = 8, FJ = 4;
+	extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+	const int lane = threadIdx.x & 63;
+	const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	const int wr = wave >> 2, wc = wave & 3;
+
+	const int tiles_m = (M + G_BM - 1) / G_BM, tiles_n = N / BN;
+	const int nwg = tiles_m * tiles_n;
+	int wg = blockIdx.x;
+	{
+		const int q = nwg / 8, rr = nwg % 8, xcd = wg % 8, idx = wg / 8;
+		wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
+	}
+	const int tm = wg % tiles_m, tn = wg / tiles_m;
+	const int row0 = tm * G_BM;
+	const int colB = tn * (BN / BMAP::COLS_PER_TILE_DIV);
+
+	// staging sources: half-tile row lr = (2 wave + i) * 8 + (lane >> 3), 16-byte chunk
+	// lane & 7 read from source chunk (lane & 7) ^ (lr & 7) (the swizzle g16frag undoes)
+	uint32_t aoff[2][2]; // [m half][i]: element offset into A
+	const uint16_t *bp[2][2];
+#pragma unroll
+	for (int i = 0; i < 2; ++i) {
+		const int lr = (2 * wave + i) * 8 + (lane >> 3);
+		const int sw = 8 * ((lane & 7) ^ (lr & 7));
+		const int ra = lr < 64 ? lr : lr + 64; // Am0 tile row; Am1 = + 64
+		aoff[0][i] = (uint32_t)min(row0 + ra, M - 1) * K + sw;
+		aoff[1][i] = (uint32_t)min(row0 + ra + 64, M - 1) * K + sw;
+		const int rb = (lr >> 5) * 64 + (lr & 31); // Bn0 tile row; Bn1 = + 32
+		bp[0][i] = bm.row(colB, rb, K) + sw;
+		bp[1][i] = bm.row(colB, rb + 32, K) + sw;
+	}
+	// half-tile h (0 Am0, 1 Am1, 2 Bn0, 3 Bn1) of K tile kt into buffer buf
+	auto stage = [&](int buf, int h, int kt) {
+		YALM_LDS void *dst0 = (YALM_LDS void *)(smem + (buf * 4 + h) * P8_HT + (2 * wave) * 8 * G_BK);
+		YALM_LDS void *dst1 = (YALM_LDS void *)(smem + (buf * 4 + h) * P8_HT + (2 * wave + 1) * 8 * G_BK);
+		const int k0 = kt * G_BK;
+		if (h < 2) {
+			__builtin_amdgcn_global_load_lds((const void *)(A + aoff[h][0] + k0), dst0, 16, 0, 0);
+			__builtin_amdgcn_global_load_lds((const void *)(A + aoff[h][1] + k0), dst1, 16, 0, 0);
+		} else {
+			__builtin_amdgcn_global_load_lds((const void *)(bp[h - 2][0] + k0), dst0, 16, 0, 0);
+			__builtin_amdgcn_global_load_lds((const void *)(bp[h - 2][1] + k0), dst1, 16, 0, 0);
+		}
+	};
+
+	f32x4_t acc[FI][FJ];
+#pragma unroll
+	for (int i = 0; i < FI; ++i)
+#pragma unroll
+		for (int j = 0; j < FJ; ++j)
+			acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+	half8_t a[4][2], b0[2][2], b1[2][2];
+
+	const int nk = K / G_BK;
+	// prologue = the previous iteration's stages p3 .. p8 for K tiles 0 (E) and 1 (O)
+	const int k1 = nk > 1 ? 1 : 0;
+	stage(0, 0, 0);
+	stage(0, 2, 0);
+	stage(0, 3, 0);
+	stage(0, 1, 0);
+	stage(1, 0, k1);
+	stage(1, 2, k1);
+	asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); // Am0, Bn0 of K tile 0
+	asm volatile("s_barrier" ::: "memory");
+	if (wr == 1)
+		asm volatile("s_barrier" ::: "memory"); // wave row 1 runs one barrier behind
+
+	auto rd_a = [&](int buf, int mh) {
+		const uint16_t *s = smem + (buf * 4 + mh) * P8_HT;
+#pragma unroll
+		for (int i = 0; i < 4; ++i)
+#pragma unroll
+			for (int ks = 0; ks < 2; ++ks)
+				a[i][ks] = g16frag(s, wr * 64 + 16 * i + (lane & 15), ks, lane);
+	};
+	auto rd_b = [&](half8_t (&b)[2][2], int buf, int nh) {
+		const uint16_t *s = smem + (buf * 4 + 2 + nh) * P8_HT;
+#pragma unroll
+		for (int j = 0; j < 2; ++j)
+#pragma unroll
+			for (int ks = 0; ks < 2; ++ks)
+				b[j][ks] = g16frag(s, wc * 32 + 16 * j + (lane & 15), ks, lane);
+	};
+	// {stage (or drain), barrier, 16 MFMAs on quadrant (mh, nh), barrier}
+	auto phase = [&](int sbuf, int sh, int skt, int mh, int nh, half8_t (&b)[2][2]) {
+		if (skt < nk) {
+			stage(sbuf, sh, skt);
+			asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+		} else {
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		}
+		asm volatile("s_barrier" ::: "memory");
+		__builtin_amdgcn_sched_barrier(0);
+		__builtin_amdgcn_s_setprio(1);
+#pragma unroll
+		for (int i = 0; i < 4; ++i)
+#pragma unroll
+			for (int j = 0; j < 2; ++j)
+#pragma unroll
+				for (int ks = 0; ks < 2; ++ks)
+					acc[4 * mh + i][2 * nh + j] =
+					    __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i][ks], b[j][ks], acc[4 * mh + i][2 * nh + j], 0, 0, 0);
+		__builtin_amdgcn_s_setprio(0);
+		__builtin_amdgcn_sched_barrier(0);
+		asm volatile("s_barrier" ::: "memory");
+	};
+
+	for (int it = 0;; ++it) {
+		const int ke = 2 * it, ko = 2 * it + 1;
+		// K tile ke from E
+		rd_a(0, 0);
+		rd_b(b0, 0, 0);
+		phase(1, 3, ko, 0, 0, b0); // p1: Bn1 O(2i+1)
+		rd_b(b1, 0, 1);
+		phase(1, 1, ko, 0, 1, b1); // p2: Am1 O(2i+1)
+		rd_a(0, 1);
+		phase(0, 0, ke + 2, 1, 1, b1); // p3: Am0 E(2i+2)
+		phase(0, 2, ke + 2, 1, 0, b0); // p4: Bn0 E(2i+2)
+		if (ko >= nk)
+			break;
+		// K tile ko from O
+		rd_a(1, 0);
+		rd_b(b0, 1, 0);
+		phase(0, 3, ke + 2, 0, 0, b0); // p5: Bn1 E(2i+2)
+		rd_b(b1, 1, 1);
+		phase(0, 1, ke + 2, 0, 1, b1); // p6: Am1 E(2i+2)
+		rd_a(1, 1);
+		phase(1, 0, ko + 2, 1, 1, b1); // p7: Am0 O(2i+3)
+		phase(1, 2, ko + 2, 1, 0, b0); // p8: Bn0 O(2i+3)
+		if (ke + 2 >= nk)
+			break;
+	}
+	if (wr == 0)
+		asm volatile("s_barrier" ::: "memory"); // rows back in step
+	asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+	EPI e = epi;
+	if constexpr (EPI::NEEDS_LDS)
+		e.red = (float *)smem;
+	const int n0 = BMAP::COLS_PER_TILE_DIV == 1 ? colB + wc * TN : colB + wc * (TN / 2);
+	e.template apply<FI, FJ>(acc, row0 + wr * TM, n0, lane, wc, 4);
+}
+
+constexpr size_t gemm8p_lds() { return (size_t)8 * P8_HT * sizeof(uint16_t); }
+
 } // namespace pf
