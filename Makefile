@@ -14,6 +14,11 @@ yalm_amd/libyalm_hip.so: $(HIP_OBJS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(HIP_OBJS) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 
+# prefill.hip: MFMA accumulators in arch VGPRs (no AGPR form): the attention kernel's O and
+# S^T accumulators are touched by VALU (softmax, rescale), and the AGPR form copied all 64 O
+# registers out and back on every key tile (260 registers -> 1 wave per SIMD; 175 without)
+build/prefill.o: HIPFLAGS += -mllvm -amdgpu-mfma-vgpr-form
+
 build/%.o: $(CSRC)/%.hip $(HIP_HDRS)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<

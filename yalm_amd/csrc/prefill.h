@@ -453,8 +453,10 @@ __global__ __launch_bounds__(THREADS) void attn_prefill_kernel(const uint16_t *_
 	uint16_t *const Vb = asmem + 2 * AKT * D; // [2][AKT * D]
 	const int lane = threadIdx.x & 63, l32 = lane & 31, hh = lane >> 5;
 	const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-	const int qb = gridDim.x - 1 - blockIdx.x; // heaviest (latest) query blocks first
-	const int h = blockIdx.y, g = h / (n_heads / n_kv);
+	// grid (heads, query blocks), x fastest: every head's heaviest (latest) query block
+	// is dispatched before any lighter one (longest-first over the whole causal grid)
+	const int qb = gridDim.y - 1 - blockIdx.y;
+	const int h = blockIdx.x, g = h / (n_heads / n_kv);
 	const int q_dim = n_heads * D, kv_dim = n_kv * D;
 	const int qw0 = qb * AQ + wave * 32; // this wave's first query row
 	const int qrow = qw0 + l32;          // this lane's query
@@ -495,73 +497,91 @@ __global__ __launch_bounds__(THREADS) void attn_prefill_kernel(const uint16_t *_
 		const uint16_t *Ks = Kb + cur * AKT * D;
 		const uint16_t *Vs = Vb + cur * AKT * D;
 
+		// a tile wholly past this wave's last query (the block's second diagonal tile for
+		// its first waves) adds nothing: skip its math (the wave still stages and syncs)
+		const bool live = key0 <= pos0 + qw0 + 31;
 		// ---- S^T = K Q^T: two 32-key blocks; register r of block j is key key0 + 32 j + crow(r, lane)
 		f32x16_t st[2];
-#pragma unroll
-		for (int j = 0; j < 2; ++j) {
-			st[j] = f32x16_t{};
-			const int kr = 32 * j + l32;
-#pragma unroll
-			for (int s = 0; s < D / 16; ++s) {
-				const int kcnk = 2 * s + hh;
-				const half8_t ka = *(const half8_t *)(Ks + kr * D + 8 * (kcnk ^ (kr % DCH)));
-				st[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ka, qf[s], st[j], 0, 0, 0);
-			}
-		}
-		// ---- online softmax for this lane's query (causal mask on the diagonal tiles)
-		const bool diag = key0 + AKT - 1 > pos0 + qw0;
-		float mx = -FLT_MAX;
-#pragma unroll
-		for (int j = 0; j < 2; ++j)
-#pragma unroll
-			for (int r = 0; r < 16; ++r) {
-				float v = st[j][r] * sl2;
-				if (diag && key0 + 32 * j + crow(r, lane) > qpos)
-					v = -FLT_MAX;
-				st[j][r] = v;
-				mx = fmaxf(mx, v);
-			}
-		mx = fmaxf(mx, xor32(mx)); // the other lane half holds the other 32 keys
-		const float mn = fmaxf(m, mx);
-		const float alpha = __builtin_amdgcn_exp2f(m - mn);
-		m = mn;
-		float ls = 0.0f;
 		half8_t pb[2][2]; // P^T fragments: [block j][k-step s]
+		if (live) {
 #pragma unroll
-		for (int j = 0; j < 2; ++j)
+			for (int j = 0; j < 2; ++j) {
+				st[j] = f32x16_t{};
+				const int kr = 32 * j + l32;
 #pragma unroll
-			for (int r = 0; r < 16; ++r) {
-				const float p = __builtin_amdgcn_exp2f(st[j][r] - mn);
-				ls += p;
-				pb[j][r >> 3][r & 7] = (_Float16)p;
-			}
-		ls += xor32(ls);
-		l = l * alpha + ls;
-#pragma unroll
-		for (int jd = 0; jd < D / 32; ++jd)
-			o[jd] *= alpha;
-		// ---- O^T += V^T P^T
-#pragma unroll
-		for (int j = 0; j < 2; ++j)
-#pragma unroll
-			for (int s = 0; s < 2; ++s) {
-				const int klo = 32 * j + 16 * s + 4 * hh + gq; // keys of elements 0..3 (row gq of the 4-row block)
-#pragma unroll
-				for (int jd = 0; jd < D / 32; ++jd) {
-					const int d = 32 * jd + dgrp + 4 * gp;
-					const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-					    (YALM_LDS short4_t *)(Vs + klo * D + 8 * ((d >> 3) ^ ((klo & 3) << 1)) + (d & 7)));
-					const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((YALM_LDS short4_t *)(
-					    Vs + (klo + 8) * D + 8 * ((d >> 3) ^ (((klo + 8) & 3) << 1)) + (d & 7)));
-					half8_t va;
-#pragma unroll
-					for (int e = 0; e < 4; ++e) {
-						va[e] = __builtin_bit_cast(_Float16, (short)lo[e]);
-						va[4 + e] = __builtin_bit_cast(_Float16, (short)hi[e]);
-					}
-					o[jd] = __builtin_amdgcn_mfma_f32_32x32x16_f16(va, pb[j][s], o[jd], 0, 0, 0);
+				for (int s = 0; s < D / 16; ++s) {
+					const int kcnk = 2 * s + hh;
+					const half8_t ka = *(const half8_t *)(Ks + kr * D + 8 * (kcnk ^ (kr % DCH)));
+					st[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ka, qf[s], st[j], 0, 0, 0);
 				}
 			}
+			// ---- online softmax for this lane's query. Raw scores; the 1/sqrt(D) log2(e)
+			// scale is folded into the exponent's FMA (sl2 > 0: the max commutes with it).
+			// Causal mask only on diagonal tiles (a uniform branch).
+			if (key0 + AKT - 1 > pos0 + qw0) {
+#pragma unroll
+				for (int j = 0; j < 2; ++j)
+#pragma unroll
+					for (int r = 0; r < 16; ++r)
+						if (key0 + 32 * j + crow(r, lane) > qpos)
+							st[j][r] = -INFINITY;
+			}
+			float mx = st[0][0];
+#pragma unroll
+			for (int j = 0; j < 2; ++j)
+#pragma unroll
+				for (int r = (j == 0 ? 1 : 0); r < 16; ++r)
+					mx = fmaxf(mx, st[j][r]);
+			mx = fmaxf(mx, xor32(mx)) * sl2; // the other lane half holds the other 32 keys
+			// deferred rescale (cdna_hip_programming.md T13): while no query's max grows by
+			// more than 2^RESCALE_LOG2 the old max stays the reference (P <= 2^8, exact
+			// enough in f16; l and O are f32); otherwise every lane moves to its new max.
+			// The decision precedes this tile's exponentials, so nothing is scaled twice.
+			if (!__all(mx - m <= 8.0f)) {
+				const float mn = fmaxf(m, mx);
+				const float alpha = __builtin_amdgcn_exp2f(m - mn);
+				m = mn;
+				l *= alpha;
+#pragma unroll
+				for (int jd = 0; jd < D / 32; ++jd)
+					o[jd] *= alpha;
+			}
+			float ls = 0.0f;
+#pragma unroll
+			for (int j = 0; j < 2; ++j)
+#pragma unroll
+				for (int r = 0; r < 16; ++r) {
+					const float p = __builtin_amdgcn_exp2f(fmaf(st[j][r], sl2, -m));
+					ls += p;
+					pb[j][r >> 3][r & 7] = (_Float16)p;
+				}
+			ls += xor32(ls);
+			l += ls;
+		}
+		// ---- O^T += V^T P^T
+		if (live) {
+#pragma unroll
+			for (int j = 0; j < 2; ++j)
+#pragma unroll
+				for (int s = 0; s < 2; ++s) {
+					const int klo = 32 * j + 16 * s + 4 * hh + gq; // keys of elements 0..3 (row gq of the 4-row block)
+#pragma unroll
+					for (int jd = 0; jd < D / 32; ++jd) {
+						const int d = 32 * jd + dgrp + 4 * gp;
+						const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+						    (YALM_LDS short4_t *)(Vs + klo * D + 8 * ((d >> 3) ^ ((klo & 3) << 1)) + (d & 7)));
+						const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((YALM_LDS short4_t *)(
+						    Vs + (klo + 8) * D + 8 * ((d >> 3) ^ (((klo + 8) & 3) << 1)) + (d & 7)));
+						half8_t va;
+#pragma unroll
+						for (int e = 0; e < 4; ++e) {
+							va[e] = __builtin_bit_cast(_Float16, (short)lo[e]);
+							va[4 + e] = __builtin_bit_cast(_Float16, (short)hi[e]);
+						}
+						o[jd] = __builtin_amdgcn_mfma_f32_32x32x16_f16(va, pb[j][s], o[jd], 0, 0, 0);
+					}
+				}
+		}
 		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 		__syncthreads(); // next tile landed; this tile's K / V reads are done
 		cur ^= 1;

@@ -187,7 +187,7 @@ pf::BSrc one(const void *w, int rows) {
 
 int launch_attn_prefill(const uint16_t *Q, const uint16_t *kc, const uint16_t *vc, int T, int pos0, int n_heads,
                         int n_kv, int head_dim, uint16_t *O, hipStream_t st) {
-	const dim3 grid((T + pf::AQ - 1) / pf::AQ, n_heads);
+	const dim3 grid(n_heads, (T + pf::AQ - 1) / pf::AQ); // heads fastest: longest-first dispatch
 	static bool attr_set = false;
 	if (!attr_set) {
 		HIPCHK(hipFuncSetAttribute((const void *)pf::attn_prefill_kernel<128>,
