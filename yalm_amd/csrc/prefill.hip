@@ -85,8 +85,9 @@ int g16_form(int kind) {
 	return f;
 }
 
-// The 256 x 256 tile runs the 8-phase schedule (prefill_gemm.h gemm8p_kernel) unless
-// YALM_PF_8P=0 (read per launch, for A/B runs and the exactness tests of both forms).
+// The 256-row tiles of width 192, 256 and 320 run the 8-phase schedule (prefill_gemm.h
+// gemm8p_kernel) unless YALM_PF_8P=0 (read per launch, for A/B runs and the exactness
+// tests of both forms).
 bool use_8phase() {
 	const char *e = getenv("YALM_PF_8P");
 	return !e || atoi(e) != 0;
@@ -111,10 +112,10 @@ int pick_bn(int form, int M, int n_eff, bool glu) {
 		if (n_eff % bn || (glu && bn != 128 && bn != 256))
 			continue;
 		const long rounds = (tiles_m * (n_eff / bn) + ncu - 1) / ncu;
-		// the 8-phase 256 x 256 tile costs 3/4 of a 2-phase tile of the same width
-		// (Llama-3B T 4096, one process: Wo / W2 at 256 in the 8-phase kernel beat
+		// an 8-phase tile (widths 192, 256) costs 3/4 of a 2-phase tile of the same
+		// width (Llama-3B T 4096, one process: Wo / W2 at 256 in the 8-phase kernel beat
 		// 192 in the 2-phase one, profiles/r3_prefill_8phase.txt)
-		const long cost = rounds * (bn + 64) * (p8 && bn == 256 ? 3 : 4);
+		const long cost = rounds * (bn + 64) * (p8 && (bn == 192 || bn == 256) ? 3 : 4);
 		if (!best || cost < best_cost || (cost == best_cost && bn > best)) {
 			best = bn;
 			best_cost = cost;
@@ -123,16 +124,17 @@ int pick_bn(int form, int M, int n_eff, bool glu) {
 	return best;
 }
 
-template <class EPI, class BMAP>
+template <class EPI, class BMAP, int FJ0, int FJ1>
 int launch_g8p(const uint16_t *A, int M, int K, const BMAP &bm, int N, const EPI &epi, hipStream_t st) {
-	auto kern = pf::gemm8p_kernel<EPI, BMAP>;
-	constexpr size_t lds = pf::gemm8p_lds();
+	auto kern = pf::gemm8p_kernel<EPI, BMAP, FJ0, FJ1>;
+	constexpr size_t lds = pf::gemm8p_lds<FJ0, FJ1>();
+	constexpr int BN = 64 * (FJ0 + FJ1);
 	static bool attr = false;
 	if (!attr) {
 		HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
 		attr = true;
 	}
-	const int nwg = ((M + pf::G_BM - 1) / pf::G_BM) * (N / 256);
+	const int nwg = ((M + pf::G_BM - 1) / pf::G_BM) * (N / BN);
 	hipLaunchKernelGGL(kern, dim3(nwg), dim3(pf::G_THREADS), lds, st, A, M, K, bm, N, epi);
 	HIPCHK(hipGetLastError());
 	return YALM_OK;
@@ -140,9 +142,11 @@ int launch_g8p(const uint16_t *A, int M, int K, const BMAP &bm, int N, const EPI
 
 template <class EPI, class BMAP, int BN, int WM>
 int launch_g16_t(const uint16_t *A, int M, int K, const BMAP &bm, int N, const EPI &epi, hipStream_t st) {
-	if constexpr (BN == 256 && WM == 2) {
-		if (use_8phase())
-			return launch_g8p<EPI, BMAP>(A, M, K, bm, N, epi, st);
+	if (use_8phase()) { // the 8-phase schedule at the same tile width (320: spills, stays 2-phase)
+		if constexpr (BN == 256 && WM == 2)
+			return launch_g8p<EPI, BMAP, 2, 2>(A, M, K, bm, N, epi, st);
+		if constexpr (BN == 192 && WM == 2)
+			return launch_g8p<EPI, BMAP, 2, 1>(A, M, K, bm, N, epi, st);
 	}
 	auto kern = pf::gemm16_kernel<EPI, BMAP, BN, WM>;
 	constexpr size_t lds = pf::gemm16_lds<BN>();

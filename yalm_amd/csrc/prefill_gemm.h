@@ -386,12 +386,22 @@ constexpr size_t gemm16_lds() {
 //       s + 4 (row 1: before barrier 2s + 8) and first read at phase >= s + 5 (row 0:
 //       after barrier 2s + 8).
 // * Tail: phases whose K tile is past the end stage nothing and wait vmcnt(0).
-constexpr int P8_HT = 128 * G_BK; // f16 per half-tile
+// * Tile widths: a wave's TN = 16 (FJ0 + FJ1) columns are split into the quadrant
+//   column halves n0 (16 FJ0) and n1 (16 FJ1): BN = 4 TN = 256 (2, 2), 192 (2, 1)
+//   (320 = (3, 2) would spill: 256 registers + scratch). Bn0 / Bn1 are 64 FJ0 / 64 FJ1 rows (FJ0 / FJ1 LDS-DMAs per thread); a
+//   window of 4 consecutive phases always holds one stage of each half-tile, so the
+//   count left in flight is the same at every phase: FJ0 + FJ1 + 4.
+constexpr int P8_HT = 128 * G_BK; // f16 per A half-tile (128 rows)
 
-template <class EPI, class BMAP>
+template <class EPI, class BMAP, int FJ0 = 2, int FJ1 = 2>
 __global__ __launch_bounds__(G_THREADS, 1) void gemm8p_kernel(const uint16_t *__restrict__ A, int M, int K, BMAP bm,
                                                              int N, EPI epi) {
-	constexpr int BN = 256, TM = 128, TN = 64, FI = 8, FJ = 4;
+	constexpr int FI = 8, FJ = FJ0 + FJ1, TM = 128, TN = 16 * FJ, BN = 4 * TN;
+	constexpr int HB0 = 64 * FJ0 * G_BK, HB1 = 64 * FJ1 * G_BK; // f16 per B half-tile
+	constexpr int OFF[4] = {0, P8_HT, 2 * P8_HT, 2 * P8_HT + HB0}; // Am0, Am1, Bn0, Bn1 in a buffer
+	constexpr int BUFE = 2 * P8_HT + HB0 + HB1;
+	constexpr int INFLIGHT = FJ0 + FJ1 + 4;
+	static_assert(FJ0 >= 1 && FJ1 >= 1 && FJ0 <= 3 && FJ1 <= 3, "quadrant widths");
 	extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
 	const int lane = threadIdx.x & 63;
 	const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -408,10 +418,11 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm8p_kernel(const uint16_t *__
 	const int row0 = tm * G_BM;
 	const int colB = tn * (BN / BMAP::COLS_PER_TILE_DIV);
 
-	// staging sources: half-tile row lr = (2 wave + i) * 8 + (lane >> 3), 16-byte chunk
-	// lane & 7 read from source chunk (lane & 7) ^ (lr & 7) (the swizzle g16frag undoes)
+	// staging sources: instruction i of a half-tile covers its rows lr = (NI wave + i) * 8
+	// + (lane >> 3), 16-byte chunk lane & 7 read from source chunk (lane & 7) ^ (lr & 7)
+	// (the swizzle g16frag undoes)
 	uint32_t aoff[2][2]; // [m half][i]: element offset into A
-	const uint16_t *bp[2][2];
+	const uint16_t *bp[2][3];
 #pragma unroll
 	for (int i = 0; i < 2; ++i) {
 		const int lr = (2 * wave + i) * 8 + (lane >> 3);
@@ -419,21 +430,38 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm8p_kernel(const uint16_t *__
 		const int ra = lr < 64 ? lr : lr + 64; // Am0 tile row; Am1 = + 64
 		aoff[0][i] = (uint32_t)min(row0 + ra, M - 1) * K + sw;
 		aoff[1][i] = (uint32_t)min(row0 + ra + 64, M - 1) * K + sw;
-		const int rb = (lr >> 5) * 64 + (lr & 31); // Bn0 tile row; Bn1 = + 32
-		bp[0][i] = bm.row(colB, rb, K) + sw;
-		bp[1][i] = bm.row(colB, rb + 32, K) + sw;
+	}
+#pragma unroll
+	for (int i = 0; i < FJ0; ++i) {
+		const int lr = (FJ0 * wave + i) * 8 + (lane >> 3);
+		const int sw = 8 * ((lane & 7) ^ (lr & 7));
+		bp[0][i] = bm.row(colB, (lr / (16 * FJ0)) * TN + lr % (16 * FJ0), K) + sw;
+	}
+#pragma unroll
+	for (int i = 0; i < FJ1; ++i) {
+		const int lr = (FJ1 * wave + i) * 8 + (lane >> 3);
+		const int sw = 8 * ((lane & 7) ^ (lr & 7));
+		bp[1][i] = bm.row(colB, (lr / (16 * FJ1)) * TN + 16 * FJ0 + lr % (16 * FJ1), K) + sw;
 	}
 	// half-tile h (0 Am0, 1 Am1, 2 Bn0, 3 Bn1) of K tile kt into buffer buf
 	auto stage = [&](int buf, int h, int kt) {
-		YALM_LDS void *dst0 = (YALM_LDS void *)(smem + (buf * 4 + h) * P8_HT + (2 * wave) * 8 * G_BK);
-		YALM_LDS void *dst1 = (YALM_LDS void *)(smem + (buf * 4 + h) * P8_HT + (2 * wave + 1) * 8 * G_BK);
 		const int k0 = kt * G_BK;
+		uint16_t *base = smem + buf * BUFE + OFF[h];
 		if (h < 2) {
-			__builtin_amdgcn_global_load_lds((const void *)(A + aoff[h][0] + k0), dst0, 16, 0, 0);
-			__builtin_amdgcn_global_load_lds((const void *)(A + aoff[h][1] + k0), dst1, 16, 0, 0);
+#pragma unroll
+			for (int i = 0; i < 2; ++i)
+				__builtin_amdgcn_global_load_lds((const void *)(A + aoff[h][i] + k0),
+				                                 (YALM_LDS void *)(base + (2 * wave + i) * 8 * G_BK), 16, 0, 0);
+		} else if (h == 2) {
+#pragma unroll
+			for (int i = 0; i < FJ0; ++i)
+				__builtin_amdgcn_global_load_lds((const void *)(bp[0][i] + k0),
+				                                 (YALM_LDS void *)(base + (FJ0 * wave + i) * 8 * G_BK), 16, 0, 0);
 		} else {
-			__builtin_amdgcn_global_load_lds((const void *)(bp[h - 2][0] + k0), dst0, 16, 0, 0);
-			__builtin_amdgcn_global_load_lds((const void *)(bp[h - 2][1] + k0), dst1, 16, 0, 0);
+#pragma unroll
+			for (int i = 0; i < FJ1; ++i)
+				__builtin_amdgcn_global_load_lds((const void *)(bp[1][i] + k0),
+				                                 (YALM_LDS void *)(base + (FJ1 * wave + i) * 8 * G_BK), 16, 0, 0);
 		}
 	};
 
@@ -443,7 +471,7 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm8p_kernel(const uint16_t *__
 #pragma unroll
 		for (int j = 0; j < FJ; ++j)
 			acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-	half8_t a[4][2], b0[2][2], b1[2][2];
+	half8_t a[4][2], b0[FJ0][2], b1[FJ1][2];
 
 	const int nk = K / G_BK;
 	// prologue = the previous iteration's stages p3 .. p8 for K tiles 0 (E) and 1 (O)
@@ -454,73 +482,111 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm8p_kernel(const uint16_t *__
 	stage(0, 1, 0);
 	stage(1, 0, k1);
 	stage(1, 2, k1);
-	asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); // Am0, Bn0 of K tile 0
+	asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INFLIGHT) : "memory"); // Am0, Bn0 of K tile 0
 	asm volatile("s_barrier" ::: "memory");
 	if (wr == 1)
 		asm volatile("s_barrier" ::: "memory"); // wave row 1 runs one barrier behind
 
 	auto rd_a = [&](int buf, int mh) {
-		const uint16_t *s = smem + (buf * 4 + mh) * P8_HT;
+		const uint16_t *s = smem + buf * BUFE + OFF[mh];
 #pragma unroll
 		for (int i = 0; i < 4; ++i)
 #pragma unroll
 			for (int ks = 0; ks < 2; ++ks)
 				a[i][ks] = g16frag(s, wr * 64 + 16 * i + (lane & 15), ks, lane);
 	};
-	auto rd_b = [&](half8_t (&b)[2][2], int buf, int nh) {
-		const uint16_t *s = smem + (buf * 4 + 2 + nh) * P8_HT;
+	auto rd_b0 = [&](int buf) {
+		const uint16_t *s = smem + buf * BUFE + OFF[2];
 #pragma unroll
-		for (int j = 0; j < 2; ++j)
+		for (int j = 0; j < FJ0; ++j)
 #pragma unroll
 			for (int ks = 0; ks < 2; ++ks)
-				b[j][ks] = g16frag(s, wc * 32 + 16 * j + (lane & 15), ks, lane);
+				b0[j][ks] = g16frag(s, wc * 16 * FJ0 + 16 * j + (lane & 15), ks, lane);
 	};
-	// {stage (or drain), barrier, 16 MFMAs on quadrant (mh, nh), barrier}
-	auto phase = [&](int sbuf, int sh, int skt, int mh, int nh, half8_t (&b)[2][2]) {
+	auto rd_b1 = [&](int buf) {
+		const uint16_t *s = smem + buf * BUFE + OFF[3];
+#pragma unroll
+		for (int j = 0; j < FJ1; ++j)
+#pragma unroll
+			for (int ks = 0; ks < 2; ++ks)
+				b1[j][ks] = g16frag(s, wc * 16 * FJ1 + 16 * j + (lane & 15), ks, lane);
+	};
+	// {stage (or drain), barrier, MFMAs on quadrant (mh, nh), barrier}
+	auto sync_stage = [&](int sbuf, int sh, int skt) {
 		if (skt < nk) {
 			stage(sbuf, sh, skt);
-			asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+			asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INFLIGHT) : "memory");
 		} else {
 			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 		}
 		asm volatile("s_barrier" ::: "memory");
 		__builtin_amdgcn_sched_barrier(0);
 		__builtin_amdgcn_s_setprio(1);
-#pragma unroll
-		for (int i = 0; i < 4; ++i)
-#pragma unroll
-			for (int j = 0; j < 2; ++j)
-#pragma unroll
-				for (int ks = 0; ks < 2; ++ks)
-					acc[4 * mh + i][2 * nh + j] =
-					    __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i][ks], b[j][ks], acc[4 * mh + i][2 * nh + j], 0, 0, 0);
+	};
+	auto sync_end = [&]() {
 		__builtin_amdgcn_s_setprio(0);
 		__builtin_amdgcn_sched_barrier(0);
 		asm volatile("s_barrier" ::: "memory");
+	};
+	auto mfma_n0 = [&](int mh) {
+#pragma unroll
+		for (int i = 0; i < 4; ++i)
+#pragma unroll
+			for (int j = 0; j < FJ0; ++j)
+#pragma unroll
+				for (int ks = 0; ks < 2; ++ks)
+					acc[4 * mh + i][j] =
+					    __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i][ks], b0[j][ks], acc[4 * mh + i][j], 0, 0, 0);
+	};
+	auto mfma_n1 = [&](int mh) {
+#pragma unroll
+		for (int i = 0; i < 4; ++i)
+#pragma unroll
+			for (int j = 0; j < FJ1; ++j)
+#pragma unroll
+				for (int ks = 0; ks < 2; ++ks)
+					acc[4 * mh + i][FJ0 + j] =
+					    __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i][ks], b1[j][ks], acc[4 * mh + i][FJ0 + j], 0, 0, 0);
 	};
 
 	for (int it = 0;; ++it) {
 		const int ke = 2 * it, ko = 2 * it + 1;
 		// K tile ke from E
 		rd_a(0, 0);
-		rd_b(b0, 0, 0);
-		phase(1, 3, ko, 0, 0, b0); // p1: Bn1 O(2i+1)
-		rd_b(b1, 0, 1);
-		phase(1, 1, ko, 0, 1, b1); // p2: Am1 O(2i+1)
+		rd_b0(0);
+		sync_stage(1, 3, ko); // p1: Bn1 O(2i+1)
+		mfma_n0(0);
+		sync_end();
+		rd_b1(0);
+		sync_stage(1, 1, ko); // p2: Am1 O(2i+1)
+		mfma_n1(0);
+		sync_end();
 		rd_a(0, 1);
-		phase(0, 0, ke + 2, 1, 1, b1); // p3: Am0 E(2i+2)
-		phase(0, 2, ke + 2, 1, 0, b0); // p4: Bn0 E(2i+2)
+		sync_stage(0, 0, ke + 2); // p3: Am0 E(2i+2)
+		mfma_n1(1);
+		sync_end();
+		sync_stage(0, 2, ke + 2); // p4: Bn0 E(2i+2)
+		mfma_n0(1);
+		sync_end();
 		if (ko >= nk)
 			break;
 		// K tile ko from O
 		rd_a(1, 0);
-		rd_b(b0, 1, 0);
-		phase(0, 3, ke + 2, 0, 0, b0); // p5: Bn1 E(2i+2)
-		rd_b(b1, 1, 1);
-		phase(0, 1, ke + 2, 0, 1, b1); // p6: Am1 E(2i+2)
+		rd_b0(1);
+		sync_stage(0, 3, ke + 2); // p5: Bn1 E(2i+2)
+		mfma_n0(0);
+		sync_end();
+		rd_b1(1);
+		sync_stage(0, 1, ke + 2); // p6: Am1 E(2i+2)
+		mfma_n1(0);
+		sync_end();
 		rd_a(1, 1);
-		phase(1, 0, ko + 2, 1, 1, b1); // p7: Am0 O(2i+3)
-		phase(1, 2, ko + 2, 1, 0, b0); // p8: Bn0 O(2i+3)
+		sync_stage(1, 0, ko + 2); // p7: Am0 O(2i+3)
+		mfma_n1(1);
+		sync_end();
+		sync_stage(1, 2, ko + 2); // p8: Bn0 O(2i+3)
+		mfma_n0(1);
+		sync_end();
 		if (ke + 2 >= nk)
 			break;
 	}
@@ -534,6 +600,9 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm8p_kernel(const uint16_t *__
 	e.template apply<FI, FJ>(acc, row0 + wr * TM, n0, lane, wc, 4);
 }
 
-constexpr size_t gemm8p_lds() { return (size_t)8 * P8_HT * sizeof(uint16_t); }
+template <int FJ0 = 2, int FJ1 = 2>
+constexpr size_t gemm8p_lds() {
+	return (size_t)2 * (2 * P8_HT + 64 * (FJ0 + FJ1) * G_BK) * sizeof(uint16_t);
+}
 
 } // namespace pf
