@@ -43,7 +43,8 @@ def test_gemm_exact_integers(M_, N, K):
 # 128 x 256 ("wide") tile; read per launch from the environment
 # (the 128-tile forms switch the large-tile kernel off: YALM_PF_G16=0); "g16-256" /
 # "g16-128": prefill_gemm.h gemm16_kernel with 256 x 256 / 256 x 128 tiles everywhere
-# ("g16-256" / "g16-192" run the 8-phase gemm8p_kernel, "-2ph" the 2-phase gemm16_kernel)
+# ("g16-256" / "g16-192" / "g16-128" run the 8-phase gemm8p_kernel, "-2ph" the 2-phase
+# gemm16_kernel; "qkv-split": the QKV GEMM as a q launch and a k | v launch from column q_dim)
 G16_ALL = "qkv:{0},wo:{0},glu:{0},w2:{0},cls:{0},test:{0}"
 FORMS = {"auto": {}, "s2": {"YALM_PF_STAGES": "2", "YALM_PF_G16": "0"}, "s3": {"YALM_PF_STAGES": "3", "YALM_PF_G16": "0"},
          "s3-wide": {"YALM_PF_STAGES": "3", "YALM_PF_WIDE": "1", "YALM_PF_G16": "0"},
@@ -53,6 +54,8 @@ FORMS = {"auto": {}, "s2": {"YALM_PF_STAGES": "2", "YALM_PF_G16": "0"}, "s3": {"
          "g16-256-2ph": {"YALM_PF_G16": G16_ALL.format(256), "YALM_PF_8P": "0"}, "g16-128": {"YALM_PF_G16": G16_ALL.format(128)},
          "g16-192": {"YALM_PF_G16": G16_ALL.format(192)},
          "g16-192-2ph": {"YALM_PF_G16": G16_ALL.format(192), "YALM_PF_8P": "0"},
+         "g16-128-2ph": {"YALM_PF_G16": G16_ALL.format(128), "YALM_PF_8P": "0"},
+         "qkv-split": {"YALM_PF_QKV_SPLIT": "1"},
          "g16-320": {"YALM_PF_G16": G16_ALL.format(320)}}
 
 
@@ -133,8 +136,8 @@ CFGS = {
 
 
 @pytest.mark.parametrize("cfg_name", ["gqa-d128", "d768"])
-@pytest.mark.parametrize("form", ["auto", "s3", "s2-wide", "g16-256", "g16-256-2ph", "g16-128", "g16-192", "g16-192-2ph",
-                                  "g16-320"])
+@pytest.mark.parametrize("form", ["auto", "s3", "s2-wide", "g16-256", "g16-256-2ph", "g16-128", "g16-128-2ph", "g16-192",
+                                  "g16-192-2ph", "g16-320", "qkv-split"])
 def test_prefill_forms_match_decode(form, cfg_name, monkeypatch):
     """The whole prefill in each GEMM form (the wide tile on every GEMM with N %
     256 == 0, incl. the vocab-tiled logits epilogue run once per column half)."""

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <type_traits>
 #include <vector>
 
 #include "decoder.h"
@@ -94,7 +95,7 @@ bool use_8phase() {
 }
 
 // BN for a GEMM of M x N (n_eff = B rows: 2 x hidden for the GLU); 0 = none fits
-int pick_bn(int form, int M, int n_eff, bool glu) {
+int pick_bn(int form, int M, int n_eff, bool glu, long *cost_out = nullptr) {
 	static const int cands[4] = {128, 192, 256, 320};
 	if (form == 0)
 		return 0;
@@ -121,11 +122,13 @@ int pick_bn(int form, int M, int n_eff, bool glu) {
 			best_cost = cost;
 		}
 	}
+	if (cost_out)
+		*cost_out = best_cost;
 	return best;
 }
 
 template <class EPI, class BMAP, int FJ0, int FJ1>
-int launch_g8p(const uint16_t *A, int M, int K, const BMAP &bm, int N, const EPI &epi, hipStream_t st) {
+int launch_g8p(const uint16_t *A, int M, int K, const BMAP &bm, int N, const EPI &epi, hipStream_t st, int c0) {
 	auto kern = pf::gemm8p_kernel<EPI, BMAP, FJ0, FJ1>;
 	constexpr size_t lds = pf::gemm8p_lds<FJ0, FJ1>();
 	constexpr int BN = 64 * (FJ0 + FJ1);
@@ -135,18 +138,25 @@ int launch_g8p(const uint16_t *A, int M, int K, const BMAP &bm, int N, const EPI
 		attr = true;
 	}
 	const int nwg = ((M + pf::G_BM - 1) / pf::G_BM) * (N / BN);
-	hipLaunchKernelGGL(kern, dim3(nwg), dim3(pf::G_THREADS), lds, st, A, M, K, bm, N, epi);
+	hipLaunchKernelGGL(kern, dim3(nwg), dim3(pf::G_THREADS), lds, st, A, M, K, bm, N, epi, c0);
 	HIPCHK(hipGetLastError());
 	return YALM_OK;
 }
 
+// c0: first output column of the launch (8-phase kernel only; the 2-phase kernels start at 0)
 template <class EPI, class BMAP, int BN, int WM>
-int launch_g16_t(const uint16_t *A, int M, int K, const BMAP &bm, int N, const EPI &epi, hipStream_t st) {
+int launch_g16_t(const uint16_t *A, int M, int K, const BMAP &bm, int N, const EPI &epi, hipStream_t st, int c0 = 0) {
 	if (use_8phase()) { // the 8-phase schedule at the same tile width (320: spills, stays 2-phase)
 		if constexpr (BN == 256 && WM == 2)
-			return launch_g8p<EPI, BMAP, 2, 2>(A, M, K, bm, N, epi, st);
+			return launch_g8p<EPI, BMAP, 2, 2>(A, M, K, bm, N, epi, st, c0);
 		if constexpr (BN == 192 && WM == 2)
-			return launch_g8p<EPI, BMAP, 2, 1>(A, M, K, bm, N, epi, st);
+			return launch_g8p<EPI, BMAP, 2, 1>(A, M, K, bm, N, epi, st, c0);
+		if constexpr (BN == 128 && std::is_same<BMAP, pf::BRowsPlain>::value) // GLU rows pair per 64-col wave
+			return launch_g8p<EPI, BMAP, 1, 1>(A, M, K, bm, N, epi, st, c0);
+	}
+	if (c0 != 0) {
+		set_err("prefill GEMM: a column offset needs the 8-phase kernel");
+		return YALM_ERR_UNSUPPORTED;
 	}
 	auto kern = pf::gemm16_kernel<EPI, BMAP, BN, WM>;
 	constexpr size_t lds = pf::gemm16_lds<BN>();
@@ -165,18 +175,18 @@ int launch_g16_t(const uint16_t *A, int M, int K, const BMAP &bm, int N, const E
 // when bn is 0 (the caller launches gemm_nt_kernel).
 template <class EPI>
 int launch_g16_plain(int bn, const uint16_t *A, int M, int K, const pf::BSrc &b, int N, const EPI &epi,
-                     hipStream_t st, bool &done) {
+                     hipStream_t st, bool &done, int c0 = 0) {
 	pf::BRowsPlain bm{b};
 	done = true;
 	switch (bn) {
 	case 128:
-		return launch_g16_t<EPI, pf::BRowsPlain, 128, 4>(A, M, K, bm, N, epi, st);
+		return launch_g16_t<EPI, pf::BRowsPlain, 128, 4>(A, M, K, bm, N, epi, st, c0);
 	case 192:
-		return launch_g16_t<EPI, pf::BRowsPlain, 192, 2>(A, M, K, bm, N, epi, st);
+		return launch_g16_t<EPI, pf::BRowsPlain, 192, 2>(A, M, K, bm, N, epi, st, c0);
 	case 256:
-		return launch_g16_t<EPI, pf::BRowsPlain, 256, 2>(A, M, K, bm, N, epi, st);
+		return launch_g16_t<EPI, pf::BRowsPlain, 256, 2>(A, M, K, bm, N, epi, st, c0);
 	case 320:
-		return launch_g16_t<EPI, pf::BRowsPlain, 320, 2>(A, M, K, bm, N, epi, st);
+		return launch_g16_t<EPI, pf::BRowsPlain, 320, 2>(A, M, K, bm, N, epi, st, c0);
 	}
 	done = false;
 	return YALM_OK;
@@ -311,8 +321,28 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 				e.head_dim = c.head_dim;
 				e.pos0 = pos0;
 				e.clip = c.qkv_clip;
-				TRY(launch_g16_plain(pick_bn(g16_form(PG_QKV), T, q_dim + 2 * kv_dim, false), b.Xn, T, c.dim, qkv,
-				                     q_dim + 2 * kv_dim, e, st, done));
+				// one launch over [q | k | v], or (8-phase, auto widths) a q launch and a k | v launch
+				// when their tiles fill whole rounds better (Llama-3B T 4096: N 5120 = 16 x 320
+				// 2-phase tiles, or q 16 x 192 + k | v 16 x 128 8-phase tiles); YALM_PF_QKV_SPLIT
+				// = 0 | 1 forces (read per launch)
+				long c_one = 0, c_q = 0, c_kv = 0;
+				const int form = g16_form(PG_QKV);
+				const int bn_one = pick_bn(form, T, q_dim + 2 * kv_dim, false, &c_one);
+				int bn_q = 0, bn_kv = 0;
+				if (use_8phase() && form < 0) {
+					bn_q = pick_bn(-1, T, q_dim, false, &c_q);
+					bn_kv = pick_bn(-1, T, 2 * kv_dim, false, &c_kv);
+					if (bn_kv == 320)
+						bn_kv = 0; // the k | v launch starts at column q_dim: 8-phase widths only
+				}
+				const char *se = getenv("YALM_PF_QKV_SPLIT");
+				const bool split = bn_q && bn_kv && (se ? atoi(se) != 0 : c_q + c_kv < c_one);
+				if (split) {
+					TRY(launch_g16_plain(bn_q, b.Xn, T, c.dim, qkv, q_dim, e, st, done));
+					TRY(launch_g16_plain(bn_kv, b.Xn, T, c.dim, qkv, 2 * kv_dim, e, st, done, q_dim));
+				} else {
+					TRY(launch_g16_plain(bn_one, b.Xn, T, c.dim, qkv, q_dim + 2 * kv_dim, e, st, done));
+				}
 			}
 			pf::EpiQKV e;
 			e.q = b.Q;

@@ -387,15 +387,16 @@ constexpr size_t gemm16_lds() {
 //       after barrier 2s + 8).
 // * Tail: phases whose K tile is past the end stage nothing and wait vmcnt(0).
 // * Tile widths: a wave's TN = 16 (FJ0 + FJ1) columns are split into the quadrant
-//   column halves n0 (16 FJ0) and n1 (16 FJ1): BN = 4 TN = 256 (2, 2), 192 (2, 1)
-//   (320 = (3, 2) would spill: 256 registers + scratch). Bn0 / Bn1 are 64 FJ0 / 64 FJ1 rows (FJ0 / FJ1 LDS-DMAs per thread); a
+//   column halves n0 (16 FJ0) and n1 (16 FJ1): BN = 4 TN = 256 (2, 2), 192 (2, 1),
+//   128 (1, 1) (320 = (3, 2) would spill: 256 registers + scratch). A launch covers N
+//   columns from column c0 (the QKV GEMM runs as a q launch and a k | v launch). Bn0 / Bn1 are 64 FJ0 / 64 FJ1 rows (FJ0 / FJ1 LDS-DMAs per thread); a
 //   window of 4 consecutive phases always holds one stage of each half-tile, so the
 //   count left in flight is the same at every phase: FJ0 + FJ1 + 4.
 constexpr int P8_HT = 128 * G_BK; // f16 per A half-tile (128 rows)
 
 template <class EPI, class BMAP, int FJ0 = 2, int FJ1 = 2>
 __global__ __launch_bounds__(G_THREADS, 1) void gemm8p_kernel(const uint16_t *__restrict__ A, int M, int K, BMAP bm,
-                                                             int N, EPI epi) {
+                                                             int N, EPI epi, int c0) {
 	constexpr int FI = 8, FJ = FJ0 + FJ1, TM = 128, TN = 16 * FJ, BN = 4 * TN;
 	constexpr int HB0 = 64 * FJ0 * G_BK, HB1 = 64 * FJ1 * G_BK; // f16 per B half-tile
 	constexpr int OFF[4] = {0, P8_HT, 2 * P8_HT, 2 * P8_HT + HB0}; // Am0, Am1, Bn0, Bn1 in a buffer
@@ -416,7 +417,7 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm8p_kernel(const uint16_t *__
 	}
 	const int tm = wg % tiles_m, tn = wg / tiles_m;
 	const int row0 = tm * G_BM;
-	const int colB = tn * (BN / BMAP::COLS_PER_TILE_DIV);
+	const int colB = c0 + tn * (BN / BMAP::COLS_PER_TILE_DIV); // c0: first column of this launch
 
 	// staging sources: instruction i of a half-tile covers its rows lr = (NI wave + i) * 8
 	// + (lane >> 3), 16-byte chunk lane & 7 read from source chunk (lane & 7) ^ (lr & 7)
