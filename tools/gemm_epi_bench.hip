@@ -1,0 +1,105 @@
+// gemm_epi_bench.hip — what the prefill GEMM epilogues cost: the 8-phase kernel
+// (prefill_gemm.h gemm8p_kernel) at the Llama-3.2-3B T = 4096 shapes with its product
+// epilogue vs a null epilogue that keeps the accumulators alive (stores only on an
+// impossible value), random f16 operands, interleaved rounds in one process.
+// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form -I yalm_amd/csrc \
+//          -o tools/gemm_epi_bench tools/gemm_epi_bench.hip
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "prefill_gemm.h"
+
+struct E16Null {
+	static constexpr bool NEEDS_LDS = false;
+	float *red = nullptr;
+	float *sink;
+	template <int FI, int FJ>
+	__device__ __forceinline__ void apply(pf::f32x4_t (&acc)[FI][FJ], int, int, int lane, int, int) const {
+		float s = 0.f;
+#pragma unroll
+		for (int i = 0; i < FI; ++i)
+#pragma unroll
+			for (int j = 0; j < FJ; ++j)
+				s += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+		if (s == 1234567.0f)
+			sink[lane] = s;
+	}
+};
+
+template <class EPI, class BMAP, int FJ0, int FJ1>
+static float run(const uint16_t *A, int M, int K, BMAP bm, int N, EPI e, int iters) {
+	auto kern = pf::gemm8p_kernel<EPI, BMAP, FJ0, FJ1>;
+	constexpr size_t lds = pf::gemm8p_lds<FJ0, FJ1>();
+	hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+	const int nwg = ((M + 255) / 256) * (N / (64 * (FJ0 + FJ1)));
+	hipEvent_t e0, e1;
+	hipEventCreate(&e0);
+	hipEventCreate(&e1);
+	hipLaunchKernelGGL(kern, dim3(nwg), dim3(512), lds, 0, A, M, K, bm, N, e, 0);
+	hipEventRecord(e0, 0);
+	for (int i = 0; i < iters; ++i)
+		hipLaunchKernelGGL(kern, dim3(nwg), dim3(512), lds, 0, A, M, K, bm, N, e, 0);
+	hipEventRecord(e1, 0);
+	hipEventSynchronize(e1);
+	float ms;
+	hipEventElapsedTime(&ms, e0, e1);
+	return ms * 1e3f / iters;
+}
+
+int main() {
+	const int M = 4096;
+	const size_t maxel = (size_t)16384 * 8192;
+	std::vector<uint16_t> h(maxel);
+	srand(3);
+	for (auto &v : h) {
+		_Float16 f = (_Float16)(((float)rand() / RAND_MAX - 0.5f) * 0.1f);
+		__builtin_memcpy(&v, &f, 2);
+	}
+	uint16_t *A, *W, *H;
+	float *X, *sink;
+	hipMalloc(&A, (size_t)M * 8192 * 2);
+	hipMalloc(&W, maxel * 2);
+	hipMalloc(&H, (size_t)M * 8192 * 2);
+	hipMalloc(&X, (size_t)M * 3072 * 4);
+	hipMalloc(&sink, 256);
+	hipMemcpy(A, h.data(), (size_t)M * 8192 * 2, hipMemcpyHostToDevice);
+	hipMemcpy(W, h.data(), maxel * 2, hipMemcpyHostToDevice);
+	hipMemset(X, 0, (size_t)M * 3072 * 4);
+	pf::BSrc b{};
+	b.p[0] = b.p[1] = b.p[2] = W;
+	E16Null en;
+	en.sink = sink;
+	pf::E16Residual er;
+	er.x = X;
+	er.ldx = 3072;
+	er.M = M;
+	pf::E16Glu<1> eg;
+	eg.h = H;
+	eg.ldh = 8192;
+	eg.M = M;
+	std::vector<float> t[6];
+	for (int r = 0; r < 7; ++r) {
+		b.end[0] = b.end[1] = b.end[2] = 3072;
+		pf::BRowsPlain bp{b};
+		t[0].push_back(run<pf::E16Residual, pf::BRowsPlain, 2, 1>(A, M, 3072, bp, 3072, er, 10)); // Wo
+		t[1].push_back(run<E16Null, pf::BRowsPlain, 2, 1>(A, M, 3072, bp, 3072, en, 10));
+		t[2].push_back(run<pf::E16Residual, pf::BRowsPlain, 2, 1>(A, M, 8192, bp, 3072, er, 10)); // W2
+		t[3].push_back(run<E16Null, pf::BRowsPlain, 2, 1>(A, M, 8192, bp, 3072, en, 10));
+		pf::BRowsGlu<64> bg{W, W + (size_t)8192 * 3072};
+		t[4].push_back(run<pf::E16Glu<1>, pf::BRowsGlu<64>, 2, 2>(A, M, 3072, bg, 16384, eg, 10)); // W1|W3
+		t[5].push_back(run<E16Null, pf::BRowsGlu<64>, 2, 2>(A, M, 3072, bg, 16384, en, 10));
+	}
+	const char *nm[6] = {"Wo  residual", "Wo  null", "W2  residual", "W2  null", "GLU glu", "GLU null"};
+	const double fl[6] = {2.0 * M * 3072 * 3072, 2.0 * M * 3072 * 3072, 2.0 * M * 3072 * 8192,
+	                      2.0 * M * 3072 * 8192, 2.0 * M * 16384 * 3072, 2.0 * M * 16384 * 3072};
+	for (int i = 0; i < 6; ++i) {
+		std::sort(t[i].begin(), t[i].end());
+		const float med = t[i][t[i].size() / 2];
+		printf("%-14s median %7.1f us  min %7.1f us  %6.0f TFLOP/s\n", nm[i], med, t[i][0], fl[i] / (med * 1e-6) / 1e12);
+	}
+	return 0;
+}
