@@ -56,16 +56,19 @@ FORMS = {"auto": {}, "s2": {"YALM_PF_STAGES": "2", "YALM_PF_G16": "0"}, "s3": {"
          "g16-192-2ph": {"YALM_PF_G16": G16_ALL.format(192), "YALM_PF_8P": "0"},
          "g16-128-2ph": {"YALM_PF_G16": G16_ALL.format(128), "YALM_PF_8P": "0"},
          "qkv-split": {"YALM_PF_QKV_SPLIT": "1"},
+         "g16-256-nopersist": {"YALM_PF_G16": G16_ALL.format(256), "YALM_PF_PERSIST": "0"},
          "g16-320": {"YALM_PF_G16": G16_ALL.format(320)}}
 
 
 @pytest.mark.parametrize("form", list(FORMS))
 @pytest.mark.parametrize("M_,N,K", [(200, 256, 192), (37, 768, 128), (1, 256, 64), (513, 5120, 640), (300, 384, 64),
-                                    (513, 512, 320), (260, 768, 448), (256, 256, 576), (70, 512, 128)])
+                                    (513, 512, 320), (260, 768, 448), (256, 256, 576), (70, 512, 128),
+                                    (1100, 16384, 192)])
 def test_gemm_forms_exact(form, M_, N, K, monkeypatch):
     """Every stage count / tile form is exact on f16-exact integer data (any
     staging race or fragment-map error shows as a wrong integer); K tiles 1..10
-    (odd and even counts: the 8-phase kernel's iteration covers two K tiles)."""
+    (odd and even counts: the 8-phase kernel's iteration covers two K tiles);
+    1100 x 16384: more 256 x 256 tiles (320) than CUs, so the persistent tile loop runs."""
     for k, v in FORMS[form].items():
         monkeypatch.setenv(k, v)
     rng = np.random.default_rng(M_ + N + K)
@@ -73,7 +76,7 @@ def test_gemm_forms_exact(form, M_, N, K, monkeypatch):
     w = rng.integers(-4, 5, size=(N, K)).astype(np.float16)
     w[:, 0] += np.arange(N, dtype=np.float16) % 7
     c = rt().gemm_f16(a, w)
-    ref = a.astype(np.int64) @ w.astype(np.int64).T
+    ref = a.astype(np.float64) @ w.astype(np.float64).T  # exact: small integers
     np.testing.assert_array_equal(c, ref.astype(np.float32))
 
 
@@ -137,7 +140,7 @@ CFGS = {
 
 @pytest.mark.parametrize("cfg_name", ["gqa-d128", "d768"])
 @pytest.mark.parametrize("form", ["auto", "s3", "s2-wide", "g16-256", "g16-256-2ph", "g16-128", "g16-128-2ph", "g16-192",
-                                  "g16-192-2ph", "g16-320", "qkv-split"])
+                                  "g16-192-2ph", "g16-320", "qkv-split", "g16-256-nopersist"])
 def test_prefill_forms_match_decode(form, cfg_name, monkeypatch):
     """The whole prefill in each GEMM form (the wide tile on every GEMM with N %
     256 == 0, incl. the vocab-tiled logits epilogue run once per column half)."""

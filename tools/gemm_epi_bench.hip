@@ -30,6 +30,27 @@ struct E16Null {
 	}
 };
 
+// the 2-phase 256 x 320 kernel (gemm16_kernel), the Llama-3B QKV form
+template <class EPI>
+static float run320(const uint16_t *A, int M, int K, pf::BRowsPlain bm, int N, EPI e, int iters) {
+	auto kern = pf::gemm16_kernel<EPI, pf::BRowsPlain, 320, 2>;
+	constexpr size_t lds = pf::gemm16_lds<320>();
+	hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+	const int nwg = ((M + 255) / 256) * (N / 320);
+	hipEvent_t e0, e1;
+	hipEventCreate(&e0);
+	hipEventCreate(&e1);
+	hipLaunchKernelGGL(kern, dim3(nwg), dim3(512), lds, 0, A, M, K, bm, N, e);
+	hipEventRecord(e0, 0);
+	for (int i = 0; i < iters; ++i)
+		hipLaunchKernelGGL(kern, dim3(nwg), dim3(512), lds, 0, A, M, K, bm, N, e);
+	hipEventRecord(e1, 0);
+	hipEventSynchronize(e1);
+	float ms;
+	hipEventElapsedTime(&ms, e0, e1);
+	return ms * 1e3f / iters;
+}
+
 template <class EPI, class BMAP, int FJ0, int FJ1>
 static float run(const uint16_t *A, int M, int K, BMAP bm, int N, EPI e, int iters) {
 	auto kern = pf::gemm8p_kernel<EPI, BMAP, FJ0, FJ1>;
@@ -81,7 +102,25 @@ int main() {
 	eg.h = H;
 	eg.ldh = 8192;
 	eg.M = M;
-	std::vector<float> t[6];
+	uint16_t *Q, *KC, *VC;
+	float *rope;
+	hipMalloc(&Q, (size_t)M * 3072 * 2);
+	hipMalloc(&KC, (size_t)M * 1024 * 2);
+	hipMalloc(&VC, (size_t)M * 1024 * 2);
+	hipMalloc(&rope, (size_t)M * 64 * 2 * 4);
+	hipMemset(rope, 0, (size_t)M * 64 * 2 * 4);
+	pf::E16QKV eq;
+	eq.q = Q;
+	eq.kc = KC;
+	eq.vc = VC;
+	eq.rope = rope;
+	eq.M = M;
+	eq.q_dim = 3072;
+	eq.kv_dim = 1024;
+	eq.head_dim = 128;
+	eq.pos0 = 0;
+	eq.clip = 3.4e38f;
+	std::vector<float> t[8];
 	for (int r = 0; r < 7; ++r) {
 		b.end[0] = b.end[1] = b.end[2] = 3072;
 		pf::BRowsPlain bp{b};
@@ -92,14 +131,25 @@ int main() {
 		pf::BRowsGlu<64> bg{W, W + (size_t)8192 * 3072};
 		t[4].push_back(run<pf::E16Glu<1>, pf::BRowsGlu<64>, 2, 2>(A, M, 3072, bg, 16384, eg, 10)); // W1|W3
 		t[5].push_back(run<E16Null, pf::BRowsGlu<64>, 2, 2>(A, M, 3072, bg, 16384, en, 10));
+		pf::BSrc bq{};
+		bq.p[0] = W;
+		bq.p[1] = W + (size_t)3072 * 3072;
+		bq.p[2] = W + (size_t)4096 * 3072;
+		bq.end[0] = 3072;
+		bq.end[1] = 4096;
+		bq.end[2] = 5120;
+		t[6].push_back(run320<pf::E16QKV>(A, M, 3072, pf::BRowsPlain{bq}, 5120, eq, 10)); // QKV
+		t[7].push_back(run320<E16Null>(A, M, 3072, pf::BRowsPlain{bq}, 5120, en, 10));
 	}
-	const char *nm[6] = {"Wo  residual", "Wo  null", "W2  residual", "W2  null", "GLU glu", "GLU null"};
-	const double fl[6] = {2.0 * M * 3072 * 3072, 2.0 * M * 3072 * 3072, 2.0 * M * 3072 * 8192,
-	                      2.0 * M * 3072 * 8192, 2.0 * M * 16384 * 3072, 2.0 * M * 16384 * 3072};
-	for (int i = 0; i < 6; ++i) {
+	const char *nm[8] = {"Wo  residual", "Wo  null", "W2  residual", "W2  null", "GLU glu", "GLU null",
+	                     "QKV qkv (2ph 320)", "QKV null (2ph 320)"};
+	const double fl[8] = {2.0 * M * 3072 * 3072, 2.0 * M * 3072 * 3072, 2.0 * M * 3072 * 8192,
+	                      2.0 * M * 3072 * 8192, 2.0 * M * 16384 * 3072, 2.0 * M * 16384 * 3072,
+	                      2.0 * M * 5120 * 3072, 2.0 * M * 5120 * 3072};
+	for (int i = 0; i < 8; ++i) {
 		std::sort(t[i].begin(), t[i].end());
 		const float med = t[i][t[i].size() / 2];
-		printf("%-14s median %7.1f us  min %7.1f us  %6.0f TFLOP/s\n", nm[i], med, t[i][0], fl[i] / (med * 1e-6) / 1e12);
+		printf("%-20s median %7.1f us  min %7.1f us  %6.0f TFLOP/s\n", nm[i], med, t[i][0], fl[i] / (med * 1e-6) / 1e12);
 	}
 	return 0;
 }

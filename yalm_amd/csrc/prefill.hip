@@ -138,7 +138,12 @@ int launch_g8p(const uint16_t *A, int M, int K, const BMAP &bm, int N, const EPI
 		attr = true;
 	}
 	const int nwg = ((M + pf::G_BM - 1) / pf::G_BM) * (N / BN);
-	hipLaunchKernelGGL(kern, dim3(nwg), dim3(pf::G_THREADS), lds, st, A, M, K, bm, N, epi, c0);
+	// more tiles than CUs: one persistent workgroup per CU walks them (YALM_PF_PERSIST=0: one
+	// workgroup per tile; read per launch)
+	const char *pe = getenv("YALM_PF_PERSIST");
+	const int ncu = (int)device_cu_count();
+	const int grid = (!pe || atoi(pe) != 0) && nwg > ncu ? ncu : nwg;
+	hipLaunchKernelGGL(kern, dim3(grid), dim3(pf::G_THREADS), lds, st, A, M, K, bm, N, epi, c0);
 	HIPCHK(hipGetLastError());
 	return YALM_OK;
 }

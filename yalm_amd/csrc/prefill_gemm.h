@@ -93,19 +93,30 @@ struct E16Residual { // X[m][n] += C  (fused_matmul_add_residuals, per row)
 	float *red = nullptr;
 	float *x;
 	int ldx, M;
+	// per row fragment: all 4 FJ loads of x issued (rows clamped) before any add, the stores
+	// predicated on the row (a per-element branch around the load made hipcc wait for each
+	// load separately: E16QKV below)
 	template <int FI, int FJ>
 	__device__ __forceinline__ void apply(f32x4_t (&acc)[FI][FJ], int m0, int n0, int lane, int, int) const {
 #pragma unroll
-		for (int i = 0; i < FI; ++i)
+		for (int i = 0; i < FI; ++i) {
+			float xv[4][FJ];
+#pragma unroll
+			for (int r = 0; r < 4; ++r) {
+				const int m = min(m0 + 16 * i + crow16(r, lane), M - 1);
+#pragma unroll
+				for (int j = 0; j < FJ; ++j)
+					xv[r][j] = x[(size_t)m * ldx + n0 + 16 * j + (lane & 15)];
+			}
 #pragma unroll
 			for (int r = 0; r < 4; ++r) {
 				const int m = m0 + 16 * i + crow16(r, lane);
-				if (m >= M)
-					continue;
+				if (m < M)
 #pragma unroll
-				for (int j = 0; j < FJ; ++j)
-					x[(size_t)m * ldx + n0 + 16 * j + (lane & 15)] += acc[i][j][r];
+					for (int j = 0; j < FJ; ++j)
+						x[(size_t)m * ldx + n0 + 16 * j + (lane & 15)] = xv[r][j] + acc[i][j][r];
 			}
+		}
 	}
 };
 
@@ -138,6 +149,11 @@ struct E16Glu {
 // [q | k | v] columns: clip (infer.cpp:280-288), RoPE on (even, odd) column pairs =
 // lanes (l, l ^ 1) via DPP (infer.cpp:291-301), q -> f16 Q, k / v -> the fp16 cache
 // rows pos0 + m (fused_rope_and_cache_update, infer.cu:642-677); as EpiQKV.
+// A 16-column block never straddles q / k / v (multiples of head_dim), so the region is
+// wave-uniform per block j (a scalar branch), and a block's 4 FI (cos, sin) pairs per
+// lane are loaded unconditionally (rows clamped) before any use: with per-element
+// region / row branches hipcc waited for each table load separately (the epilogue cost
+// 71 of 172 us at Llama-3B T 4096, tools/gemm_epi_bench.hip).
 struct E16QKV {
 	static constexpr bool NEEDS_LDS = false;
 	float *red = nullptr;
@@ -151,33 +167,38 @@ struct E16QKV {
 		const bool odd = lane & 1;
 #pragma unroll
 		for (int j = 0; j < FJ; ++j) {
-			const int n = n0 + 16 * j + (lane & 15);
-			const bool is_v = n >= q_dim + kv_dim;
-			const int nn = n < q_dim ? n : (n < q_dim + kv_dim ? n - q_dim : n - q_dim - kv_dim);
+			const int nb = __builtin_amdgcn_readfirstlane(n0 + 16 * j); // block's first column
+			const int region = nb < q_dim ? 0 : (nb < q_dim + kv_dim ? 1 : 2);
+			const int base = region == 0 ? 0 : (region == 1 ? q_dim : q_dim + kv_dim);
+			const int nn = nb - base + (lane & 15); // column inside q / k / v
 			const int fj = (nn % head_dim) >> 1;
+			const bool rot = region != 2;
+			uint16_t *const dst = (region == 0 ? q : (region == 1 ? kc : vc)) + nn;
+			const int ld = region == 0 ? q_dim : kv_dim, roff = region == 0 ? 0 : pos0;
+			constexpr int IB = FI < 4 ? FI : 4; // row fragments per batch of table loads
 #pragma unroll
-			for (int i = 0; i < FI; ++i)
+			for (int i0 = 0; i0 < FI; i0 += IB) {
+				float2_t cs[IB][4];
 #pragma unroll
-				for (int r = 0; r < 4; ++r) {
-					float v = acc[i][j][r];
-					v = v < -clip ? -clip : (v > clip ? clip : v);
-					const float p = dpp<0xB1>(v); // partner column (n ^ 1)
-					const int m = m0 + 16 * i + crow16(r, lane);
-					if (m >= M)
-						continue;
-					const int pos = pos0 + m;
-					float o = v;
-					if (!is_v) {
-						const float2_t cs = *(const float2_t *)(rope + ((size_t)m * (head_dim >> 1) + fj) * 2);
-						o = odd ? p * cs[1] + v * cs[0] : v * cs[0] - p * cs[1];
+				for (int i = 0; i < IB; ++i)
+#pragma unroll
+					for (int r = 0; r < 4; ++r) {
+						const int m = min(m0 + 16 * (i0 + i) + crow16(r, lane), M - 1);
+						cs[i][r] = *(const float2_t *)(rope + ((size_t)m * (head_dim >> 1) + fj) * 2);
 					}
-					if (n < q_dim)
-						q[(size_t)m * q_dim + n] = f2h_bits(o);
-					else if (!is_v)
-						kc[(size_t)pos * kv_dim + nn] = f2h(o);
-					else
-						vc[(size_t)pos * kv_dim + nn] = f2h(o);
-				}
+#pragma unroll
+				for (int i = 0; i < IB; ++i)
+#pragma unroll
+					for (int r = 0; r < 4; ++r) {
+						float v = acc[i0 + i][j][r];
+						v = v < -clip ? -clip : (v > clip ? clip : v);
+						const float p = dpp<0xB1>(v); // partner column (n ^ 1)
+						const float ro = odd ? p * cs[i][r][1] + v * cs[i][r][0] : v * cs[i][r][0] - p * cs[i][r][1];
+						const int m = m0 + 16 * (i0 + i) + crow16(r, lane);
+						if (m < M)
+							dst[(size_t)(roff + m) * ld] = f2h(rot ? ro : v);
+					}
+			}
 		}
 	}
 };
@@ -410,195 +431,202 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm8p_kernel(const uint16_t *__
 
 	const int tiles_m = (M + G_BM - 1) / G_BM, tiles_n = N / BN;
 	const int nwg = tiles_m * tiles_n;
-	int wg = blockIdx.x;
-	{
-		const int q = nwg / 8, rr = nwg % 8, xcd = wg % 8, idx = wg / 8;
-		wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
-	}
-	const int tm = wg % tiles_m, tn = wg / tiles_m;
-	const int row0 = tm * G_BM;
-	const int colB = c0 + tn * (BN / BMAP::COLS_PER_TILE_DIV); // c0: first column of this launch
-
-	// staging sources: instruction i of a half-tile covers its rows lr = (NI wave + i) * 8
-	// + (lane >> 3), 16-byte chunk lane & 7 read from source chunk (lane & 7) ^ (lr & 7)
-	// (the swizzle g16frag undoes)
-	uint32_t aoff[2][2]; // [m half][i]: element offset into A
-	const uint16_t *bp[2][3];
-#pragma unroll
-	for (int i = 0; i < 2; ++i) {
-		const int lr = (2 * wave + i) * 8 + (lane >> 3);
-		const int sw = 8 * ((lane & 7) ^ (lr & 7));
-		const int ra = lr < 64 ? lr : lr + 64; // Am0 tile row; Am1 = + 64
-		aoff[0][i] = (uint32_t)min(row0 + ra, M - 1) * K + sw;
-		aoff[1][i] = (uint32_t)min(row0 + ra + 64, M - 1) * K + sw;
-	}
-#pragma unroll
-	for (int i = 0; i < FJ0; ++i) {
-		const int lr = (FJ0 * wave + i) * 8 + (lane >> 3);
-		const int sw = 8 * ((lane & 7) ^ (lr & 7));
-		bp[0][i] = bm.row(colB, (lr / (16 * FJ0)) * TN + lr % (16 * FJ0), K) + sw;
-	}
-#pragma unroll
-	for (int i = 0; i < FJ1; ++i) {
-		const int lr = (FJ1 * wave + i) * 8 + (lane >> 3);
-		const int sw = 8 * ((lane & 7) ^ (lr & 7));
-		bp[1][i] = bm.row(colB, (lr / (16 * FJ1)) * TN + 16 * FJ0 + lr % (16 * FJ1), K) + sw;
-	}
-	// half-tile h (0 Am0, 1 Am1, 2 Bn0, 3 Bn1) of K tile kt into buffer buf
-	auto stage = [&](int buf, int h, int kt) {
-		const int k0 = kt * G_BK;
-		uint16_t *base = smem + buf * BUFE + OFF[h];
-		if (h < 2) {
-#pragma unroll
-			for (int i = 0; i < 2; ++i)
-				__builtin_amdgcn_global_load_lds((const void *)(A + aoff[h][i] + k0),
-				                                 (YALM_LDS void *)(base + (2 * wave + i) * 8 * G_BK), 16, 0, 0);
-		} else if (h == 2) {
-#pragma unroll
-			for (int i = 0; i < FJ0; ++i)
-				__builtin_amdgcn_global_load_lds((const void *)(bp[0][i] + k0),
-				                                 (YALM_LDS void *)(base + (FJ0 * wave + i) * 8 * G_BK), 16, 0, 0);
-		} else {
-#pragma unroll
-			for (int i = 0; i < FJ1; ++i)
-				__builtin_amdgcn_global_load_lds((const void *)(bp[1][i] + k0),
-				                                 (YALM_LDS void *)(base + (FJ1 * wave + i) * 8 * G_BK), 16, 0, 0);
+	// one tile per workgroup, or (grid smaller than the tile count) a persistent loop over
+	// tiles b, b + grid, ...: the next tile's LDS-DMA prologue follows this tile's epilogue
+	// stores without a workgroup exit and dispatch in between
+	for (int t = blockIdx.x; t < nwg; t += gridDim.x) {
+		if (EPI::NEEDS_LDS && t != (int)blockIdx.x) // the previous tile's epilogue is done with LDS
+			asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); // (stores may stay in flight)
+		int wg = t;
+		{
+			const int q = nwg / 8, rr = nwg % 8, xcd = wg % 8, idx = wg / 8;
+			wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
 		}
-	};
+		const int tm = wg % tiles_m, tn = wg / tiles_m;
+		const int row0 = tm * G_BM;
+		const int colB = c0 + tn * (BN / BMAP::COLS_PER_TILE_DIV); // c0: first column of this launch
 
-	f32x4_t acc[FI][FJ];
-#pragma unroll
-	for (int i = 0; i < FI; ++i)
-#pragma unroll
-		for (int j = 0; j < FJ; ++j)
-			acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-	half8_t a[4][2], b0[FJ0][2], b1[FJ1][2];
-
-	const int nk = K / G_BK;
-	// prologue = the previous iteration's stages p3 .. p8 for K tiles 0 (E) and 1 (O)
-	const int k1 = nk > 1 ? 1 : 0;
-	stage(0, 0, 0);
-	stage(0, 2, 0);
-	stage(0, 3, 0);
-	stage(0, 1, 0);
-	stage(1, 0, k1);
-	stage(1, 2, k1);
-	asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INFLIGHT) : "memory"); // Am0, Bn0 of K tile 0
-	asm volatile("s_barrier" ::: "memory");
-	if (wr == 1)
-		asm volatile("s_barrier" ::: "memory"); // wave row 1 runs one barrier behind
-
-	auto rd_a = [&](int buf, int mh) {
-		const uint16_t *s = smem + buf * BUFE + OFF[mh];
-#pragma unroll
-		for (int i = 0; i < 4; ++i)
-#pragma unroll
-			for (int ks = 0; ks < 2; ++ks)
-				a[i][ks] = g16frag(s, wr * 64 + 16 * i + (lane & 15), ks, lane);
-	};
-	auto rd_b0 = [&](int buf) {
-		const uint16_t *s = smem + buf * BUFE + OFF[2];
-#pragma unroll
-		for (int j = 0; j < FJ0; ++j)
-#pragma unroll
-			for (int ks = 0; ks < 2; ++ks)
-				b0[j][ks] = g16frag(s, wc * 16 * FJ0 + 16 * j + (lane & 15), ks, lane);
-	};
-	auto rd_b1 = [&](int buf) {
-		const uint16_t *s = smem + buf * BUFE + OFF[3];
-#pragma unroll
-		for (int j = 0; j < FJ1; ++j)
-#pragma unroll
-			for (int ks = 0; ks < 2; ++ks)
-				b1[j][ks] = g16frag(s, wc * 16 * FJ1 + 16 * j + (lane & 15), ks, lane);
-	};
-	// {stage (or drain), barrier, MFMAs on quadrant (mh, nh), barrier}
-	auto sync_stage = [&](int sbuf, int sh, int skt) {
-		if (skt < nk) {
-			stage(sbuf, sh, skt);
-			asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INFLIGHT) : "memory");
-		} else {
-			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		// staging sources: instruction i of a half-tile covers its rows lr = (NI wave + i) * 8
+		// + (lane >> 3), 16-byte chunk lane & 7 read from source chunk (lane & 7) ^ (lr & 7)
+		// (the swizzle g16frag undoes)
+		uint32_t aoff[2][2]; // [m half][i]: element offset into A
+		const uint16_t *bp[2][3];
+	#pragma unroll
+		for (int i = 0; i < 2; ++i) {
+			const int lr = (2 * wave + i) * 8 + (lane >> 3);
+			const int sw = 8 * ((lane & 7) ^ (lr & 7));
+			const int ra = lr < 64 ? lr : lr + 64; // Am0 tile row; Am1 = + 64
+			aoff[0][i] = (uint32_t)min(row0 + ra, M - 1) * K + sw;
+			aoff[1][i] = (uint32_t)min(row0 + ra + 64, M - 1) * K + sw;
 		}
+	#pragma unroll
+		for (int i = 0; i < FJ0; ++i) {
+			const int lr = (FJ0 * wave + i) * 8 + (lane >> 3);
+			const int sw = 8 * ((lane & 7) ^ (lr & 7));
+			bp[0][i] = bm.row(colB, (lr / (16 * FJ0)) * TN + lr % (16 * FJ0), K) + sw;
+		}
+	#pragma unroll
+		for (int i = 0; i < FJ1; ++i) {
+			const int lr = (FJ1 * wave + i) * 8 + (lane >> 3);
+			const int sw = 8 * ((lane & 7) ^ (lr & 7));
+			bp[1][i] = bm.row(colB, (lr / (16 * FJ1)) * TN + 16 * FJ0 + lr % (16 * FJ1), K) + sw;
+		}
+		// half-tile h (0 Am0, 1 Am1, 2 Bn0, 3 Bn1) of K tile kt into buffer buf
+		auto stage = [&](int buf, int h, int kt) {
+			const int k0 = kt * G_BK;
+			uint16_t *base = smem + buf * BUFE + OFF[h];
+			if (h < 2) {
+	#pragma unroll
+				for (int i = 0; i < 2; ++i)
+					__builtin_amdgcn_global_load_lds((const void *)(A + aoff[h][i] + k0),
+					                                 (YALM_LDS void *)(base + (2 * wave + i) * 8 * G_BK), 16, 0, 0);
+			} else if (h == 2) {
+	#pragma unroll
+				for (int i = 0; i < FJ0; ++i)
+					__builtin_amdgcn_global_load_lds((const void *)(bp[0][i] + k0),
+					                                 (YALM_LDS void *)(base + (FJ0 * wave + i) * 8 * G_BK), 16, 0, 0);
+			} else {
+	#pragma unroll
+				for (int i = 0; i < FJ1; ++i)
+					__builtin_amdgcn_global_load_lds((const void *)(bp[1][i] + k0),
+					                                 (YALM_LDS void *)(base + (FJ1 * wave + i) * 8 * G_BK), 16, 0, 0);
+			}
+		};
+
+		f32x4_t acc[FI][FJ];
+	#pragma unroll
+		for (int i = 0; i < FI; ++i)
+	#pragma unroll
+			for (int j = 0; j < FJ; ++j)
+				acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+		half8_t a[4][2], b0[FJ0][2], b1[FJ1][2];
+
+		const int nk = K / G_BK;
+		// prologue = the previous iteration's stages p3 .. p8 for K tiles 0 (E) and 1 (O)
+		const int k1 = nk > 1 ? 1 : 0;
+		stage(0, 0, 0);
+		stage(0, 2, 0);
+		stage(0, 3, 0);
+		stage(0, 1, 0);
+		stage(1, 0, k1);
+		stage(1, 2, k1);
+		asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INFLIGHT) : "memory"); // Am0, Bn0 of K tile 0
 		asm volatile("s_barrier" ::: "memory");
-		__builtin_amdgcn_sched_barrier(0);
-		__builtin_amdgcn_s_setprio(1);
-	};
-	auto sync_end = [&]() {
-		__builtin_amdgcn_s_setprio(0);
-		__builtin_amdgcn_sched_barrier(0);
-		asm volatile("s_barrier" ::: "memory");
-	};
-	auto mfma_n0 = [&](int mh) {
-#pragma unroll
-		for (int i = 0; i < 4; ++i)
-#pragma unroll
+		if (wr == 1)
+			asm volatile("s_barrier" ::: "memory"); // wave row 1 runs one barrier behind
+
+		auto rd_a = [&](int buf, int mh) {
+			const uint16_t *s = smem + buf * BUFE + OFF[mh];
+	#pragma unroll
+			for (int i = 0; i < 4; ++i)
+	#pragma unroll
+				for (int ks = 0; ks < 2; ++ks)
+					a[i][ks] = g16frag(s, wr * 64 + 16 * i + (lane & 15), ks, lane);
+		};
+		auto rd_b0 = [&](int buf) {
+			const uint16_t *s = smem + buf * BUFE + OFF[2];
+	#pragma unroll
 			for (int j = 0; j < FJ0; ++j)
-#pragma unroll
+	#pragma unroll
 				for (int ks = 0; ks < 2; ++ks)
-					acc[4 * mh + i][j] =
-					    __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i][ks], b0[j][ks], acc[4 * mh + i][j], 0, 0, 0);
-	};
-	auto mfma_n1 = [&](int mh) {
-#pragma unroll
-		for (int i = 0; i < 4; ++i)
-#pragma unroll
+					b0[j][ks] = g16frag(s, wc * 16 * FJ0 + 16 * j + (lane & 15), ks, lane);
+		};
+		auto rd_b1 = [&](int buf) {
+			const uint16_t *s = smem + buf * BUFE + OFF[3];
+	#pragma unroll
 			for (int j = 0; j < FJ1; ++j)
-#pragma unroll
+	#pragma unroll
 				for (int ks = 0; ks < 2; ++ks)
-					acc[4 * mh + i][FJ0 + j] =
-					    __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i][ks], b1[j][ks], acc[4 * mh + i][FJ0 + j], 0, 0, 0);
-	};
+					b1[j][ks] = g16frag(s, wc * 16 * FJ1 + 16 * j + (lane & 15), ks, lane);
+		};
+		// {stage (or drain), barrier, MFMAs on quadrant (mh, nh), barrier}
+		auto sync_stage = [&](int sbuf, int sh, int skt) {
+			if (skt < nk) {
+				stage(sbuf, sh, skt);
+				asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INFLIGHT) : "memory");
+			} else {
+				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			}
+			asm volatile("s_barrier" ::: "memory");
+			__builtin_amdgcn_sched_barrier(0);
+			__builtin_amdgcn_s_setprio(1);
+		};
+		auto sync_end = [&]() {
+			__builtin_amdgcn_s_setprio(0);
+			__builtin_amdgcn_sched_barrier(0);
+			asm volatile("s_barrier" ::: "memory");
+		};
+		auto mfma_n0 = [&](int mh) {
+	#pragma unroll
+			for (int i = 0; i < 4; ++i)
+	#pragma unroll
+				for (int j = 0; j < FJ0; ++j)
+	#pragma unroll
+					for (int ks = 0; ks < 2; ++ks)
+						acc[4 * mh + i][j] =
+						    __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i][ks], b0[j][ks], acc[4 * mh + i][j], 0, 0, 0);
+		};
+		auto mfma_n1 = [&](int mh) {
+	#pragma unroll
+			for (int i = 0; i < 4; ++i)
+	#pragma unroll
+				for (int j = 0; j < FJ1; ++j)
+	#pragma unroll
+					for (int ks = 0; ks < 2; ++ks)
+						acc[4 * mh + i][FJ0 + j] =
+						    __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i][ks], b1[j][ks], acc[4 * mh + i][FJ0 + j], 0, 0, 0);
+		};
 
-	for (int it = 0;; ++it) {
-		const int ke = 2 * it, ko = 2 * it + 1;
-		// K tile ke from E
-		rd_a(0, 0);
-		rd_b0(0);
-		sync_stage(1, 3, ko); // p1: Bn1 O(2i+1)
-		mfma_n0(0);
-		sync_end();
-		rd_b1(0);
-		sync_stage(1, 1, ko); // p2: Am1 O(2i+1)
-		mfma_n1(0);
-		sync_end();
-		rd_a(0, 1);
-		sync_stage(0, 0, ke + 2); // p3: Am0 E(2i+2)
-		mfma_n1(1);
-		sync_end();
-		sync_stage(0, 2, ke + 2); // p4: Bn0 E(2i+2)
-		mfma_n0(1);
-		sync_end();
-		if (ko >= nk)
-			break;
-		// K tile ko from O
-		rd_a(1, 0);
-		rd_b0(1);
-		sync_stage(0, 3, ke + 2); // p5: Bn1 E(2i+2)
-		mfma_n0(0);
-		sync_end();
-		rd_b1(1);
-		sync_stage(0, 1, ke + 2); // p6: Am1 E(2i+2)
-		mfma_n1(0);
-		sync_end();
-		rd_a(1, 1);
-		sync_stage(1, 0, ko + 2); // p7: Am0 O(2i+3)
-		mfma_n1(1);
-		sync_end();
-		sync_stage(1, 2, ko + 2); // p8: Bn0 O(2i+3)
-		mfma_n0(1);
-		sync_end();
-		if (ke + 2 >= nk)
-			break;
+		for (int it = 0;; ++it) {
+			const int ke = 2 * it, ko = 2 * it + 1;
+			// K tile ke from E
+			rd_a(0, 0);
+			rd_b0(0);
+			sync_stage(1, 3, ko); // p1: Bn1 O(2i+1)
+			mfma_n0(0);
+			sync_end();
+			rd_b1(0);
+			sync_stage(1, 1, ko); // p2: Am1 O(2i+1)
+			mfma_n1(0);
+			sync_end();
+			rd_a(0, 1);
+			sync_stage(0, 0, ke + 2); // p3: Am0 E(2i+2)
+			mfma_n1(1);
+			sync_end();
+			sync_stage(0, 2, ke + 2); // p4: Bn0 E(2i+2)
+			mfma_n0(1);
+			sync_end();
+			if (ko >= nk)
+				break;
+			// K tile ko from O
+			rd_a(1, 0);
+			rd_b0(1);
+			sync_stage(0, 3, ke + 2); // p5: Bn1 E(2i+2)
+			mfma_n0(0);
+			sync_end();
+			rd_b1(1);
+			sync_stage(0, 1, ke + 2); // p6: Am1 E(2i+2)
+			mfma_n1(0);
+			sync_end();
+			rd_a(1, 1);
+			sync_stage(1, 0, ko + 2); // p7: Am0 O(2i+3)
+			mfma_n1(1);
+			sync_end();
+			sync_stage(1, 2, ko + 2); // p8: Bn0 O(2i+3)
+			mfma_n0(1);
+			sync_end();
+			if (ke + 2 >= nk)
+				break;
+		}
+		if (wr == 0)
+			asm volatile("s_barrier" ::: "memory"); // rows back in step
+		asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+		EPI e = epi;
+		if constexpr (EPI::NEEDS_LDS)
+			e.red = (float *)smem;
+		const int n0 = BMAP::COLS_PER_TILE_DIV == 1 ? colB + wc * TN : colB + wc * (TN / 2);
+		e.template apply<FI, FJ>(acc, row0 + wr * TM, n0, lane, wc, 4);
 	}
-	if (wr == 0)
-		asm volatile("s_barrier" ::: "memory"); // rows back in step
-	asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-	EPI e = epi;
-	if constexpr (EPI::NEEDS_LDS)
-		e.red = (float *)smem;
-	const int n0 = BMAP::COLS_PER_TILE_DIV == 1 ? colB + wc * TN : colB + wc * (TN / 2);
-	e.template apply<FI, FJ>(acc, row0 + wr * TM, n0, lane, wc, 4);
 }
 
 template <int FJ0 = 2, int FJ1 = 2>
