@@ -132,6 +132,9 @@ CFGS = {
     "small-d64": M.SMALL,
     "gqa-d128": M.ModelConfig(dim=512, hidden_dim=1024, head_dim=128, n_layers=3, n_heads=4, n_kv_heads=2,
                               vocab_size=1024, max_seq_len=320, rope_theta=1e6, act=M.SILU, weight_dtype=M.F16),
+    # GELU-tanh GLU (the prefill's fast exp2 / rcp form vs the decode's tanhf)
+    "gelu-d128": M.ModelConfig(dim=512, hidden_dim=1024, head_dim=128, n_layers=2, n_heads=4, n_kv_heads=2,
+                               vocab_size=1024, max_seq_len=320, rope_theta=1e6, act=M.GELU, weight_dtype=M.F16),
     # QKV N 1280 = 4 x 320, Wo / W2 N 768 = 4 x 192, vocab 1920 = 10 x 192: the 192 / 320 tile widths
     "d768": M.ModelConfig(dim=768, hidden_dim=1536, head_dim=128, n_layers=2, n_heads=6, n_kv_heads=2,
                           vocab_size=1920, max_seq_len=320, rope_theta=1e6, act=M.SILU, weight_dtype=M.F16),

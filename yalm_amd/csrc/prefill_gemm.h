@@ -120,6 +120,23 @@ struct E16Residual { // X[m][n] += C  (fused_matmul_add_residuals, per row)
 	}
 };
 
+// SiLU / GELU-tanh (infer.cu:586-596) with the hardware exp2 / reciprocal (1 ulp each)
+// instead of the libm-accurate expf, tanhf and IEEE division: the result is rounded to
+// f16 for the next GEMM anyway (its rounding error, 2^-11, is ~1000x these ulps), and
+// the accurate forms made the GLU epilogue ~10% of the GEMM (tools/gemm_epi_bench.hip).
+// The decode path keeps act_fn (parity bars of 1e-4 there).
+template <int ACT>
+__device__ __forceinline__ float act_fast(float x) {
+	if constexpr (ACT == 1) {
+		return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x));
+	} else {
+		const float y = 0.797885f * (x + 0.044715f * x * x * x);
+		// tanh(y) = 1 - 2 / (e^(2y) + 1); e^(2y) overflows to inf for large y -> 1
+		const float t = 1.0f - 2.0f * __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(2.8853900817779268f * y) + 1.0f);
+		return 0.5f * x * (1.0f + t);
+	}
+}
+
 // H = f16(act(X W1^T) * (X W3^T)) (fused_ffn_w1_w3_glu_act): columns j < FJ / 2 of a
 // wave are W1 outputs, j >= FJ / 2 the W3 outputs of the same hidden columns.
 // n0 here is the wave's first HIDDEN column (BRowsGlu).
@@ -141,7 +158,7 @@ struct E16Glu {
 #pragma unroll
 				for (int j = 0; j < FJ / 2; ++j)
 					h[(size_t)m * ldh + n0 + 16 * j + (lane & 15)] =
-					    f2h_bits(act_fn<ACT>(acc[i][j][r]) * acc[i][j + FJ / 2][r]);
+					    f2h_bits(act_fast<ACT>(acc[i][j][r]) * acc[i][j + FJ / 2][r]);
 			}
 	}
 };
