@@ -229,15 +229,22 @@ struct E16Logits {
 	const int *targets;
 	int M, ntiles;
 	float *red; // LDS scratch [WN][256 rows][2]
+	// The targets of a row fragment's 4 rows are loaded together (rows clamped, the store
+	// predicated: no load inside a per-element branch, see E16QKV), and exp(l - max) is the
+	// hardware exp2 on a log2(e)-scaled FMA (1 ulp, far inside the perplexity bar).
 	template <int FI, int FJ>
 	__device__ __forceinline__ void apply(f32x4_t (&acc)[FI][FJ], int m0, int n0, int lane, int wc, int wn) const {
 		const int tm0 = m0 - (m0 % G_BM); // tile's first row
+		constexpr float L2E = 1.4426950408889634f;
 #pragma unroll
 		for (int i = 0; i < FI; ++i) {
+			int tg[4];
+#pragma unroll
+			for (int r = 0; r < 4; ++r)
+				tg[r] = targets[min(m0 + 16 * i + crow16(r, lane), M - 1)];
 #pragma unroll
 			for (int r = 0; r < 4; ++r) {
 				const int m = m0 + 16 * i + crow16(r, lane);
-				const int tgt = m < M ? targets[m] : -1;
 				float mx = acc[i][0][r];
 #pragma unroll
 				for (int j = 1; j < FJ; ++j)
@@ -245,12 +252,13 @@ struct E16Logits {
 				mx = row16_max(mx); // the 16 lanes of this row group hold its 16 columns
 #pragma unroll
 				for (int j = 0; j < FJ; ++j)
-					if (n0 + 16 * j + (lane & 15) == tgt)
+					if (m < M && n0 + 16 * j + (lane & 15) == tg[r])
 						tgt_logit[m] = acc[i][j][r];
+				const float mxs = mx * L2E;
 				float s = 0.0f;
 #pragma unroll
 				for (int j = 0; j < FJ; ++j)
-					s += expf(acc[i][j][r] - mx);
+					s += __builtin_amdgcn_exp2f(fmaf(acc[i][j][r], L2E, -mxs));
 				s = row16_sum(s);
 				if ((lane & 15) == 0) {
 					const int rl = m - tm0;
