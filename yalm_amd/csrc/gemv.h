@@ -437,7 +437,13 @@ __global__ __launch_bounds__(GEMV_THREADS) void gemv_kernel(P p, const float *__
 // of L2 reads for W1/W3 before). Row partials are wave-reduced (DPP), parked
 // in LDS per (row, wave) and summed in wave order by one thread per group,
 // which runs the policy epilogue (finish_all).
-template <class WT, class P, int U, bool NORM, int THREADS>
+//
+// ROWS (chosen by the launcher when every workgroup's virtual rows divide evenly over its
+// waves: W1|W3, W2): whole rows are dealt round-robin instead, each wave streaming all
+// chunks of its rows, so the wave reduction runs once per row instead of once per 1-KB
+// chunk (W1|W3 at n 4096: 8 reductions per row -> 1; tools/pattern_bench.hip: the chunk
+// order with its per-chunk work ran 10-25% below the streaming envelope, whole rows at it).
+template <class WT, class P, int U, bool NORM, int THREADS, bool ROWS = false>
 __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__restrict__ x,
                                                           const float *__restrict__ normw, float eps) {
 	extern __shared__ __attribute__((aligned(16))) float xs[];
@@ -454,7 +460,8 @@ __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__re
 	const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 	const int ngl = b < p.n_groups ? (p.n_groups - 1 - b) / NB + 1 : 0; // groups of this workgroup
 	const int items = ngl * R * nch;
-	const int mine = items > wave ? (items - 1 - wave) / W + 1 : 0; // items wave, wave + W, ...
+	const int mine = ROWS ? (ngl * R > wave ? ((ngl * R - 1 - wave) / W + 1) * nch : 0) // rows wave, wave + W, ...
+	                      : (items > wave ? (items - 1 - wave) / W + 1 : 0);            // items wave, wave + W, ...
 	float *part = xs + ((n + 3) & ~3) + 64;                         // [ngl * R][W]
 	const size_t lane_off = (size_t)lane * EPL * WT::BYTES;
 	const char *dummy = (const char *)x + lane * 16;
@@ -463,10 +470,17 @@ __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__re
 #endif
 
 	auto advance = [&](int &vr, int &c) {
-		c += W;
-		while (c >= nch) {
-			c -= nch;
-			++vr;
+		if constexpr (ROWS) {
+			if (++c == nch) {
+				c = 0;
+				vr += W;
+			}
+		} else {
+			c += W;
+			while (c >= nch) {
+				c -= nch;
+				++vr;
+			}
 		}
 	};
 	auto iaddr = [&](int vr, int c) {
@@ -475,7 +489,7 @@ __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__re
 	};
 	auto pslot = [&](int vr) { return vr * W + wave; }; // LDS partial slot of item row vr
 
-	int ivr = wave / nch, ic = wave - (wave / nch) * nch; // issue cursor
+	int ivr = ROWS ? wave : wave / nch, ic = ROWS ? 0 : wave - (wave / nch) * nch; // issue cursor
 	const int vr0 = ivr, c0 = ic;
 	const bool xregs = n <= 4 * xpre_n<NORM>() * THREADS; // x (+ norm weights) fit the registers
 	XPre<NORM> xp;

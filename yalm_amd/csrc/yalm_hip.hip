@@ -128,11 +128,48 @@ int device_cu_count() {
 
 // Row-block geometry (gemv_rb_kernel): `gpw` = workgroups per CU (default 1),
 // threads 512 (8 waves), U = 8 loads in flight per wave.
+// whole-row mode (gemv.h ROWS): W1|W3 (PGlu), W2 / Wo (PResidual), QKV (PQKV) when the rows divide
+// evenly over the waves
+template <class P>
+struct RowsMode {
+	static constexpr bool value = false;
+};
+template <class WT, int ACT>
+struct RowsMode<PGlu<WT, ACT>> {
+	static constexpr bool value = true;
+};
+template <class WT, int R>
+struct RowsMode<PResidual<WT, R>> {
+	static constexpr bool value = true;
+};
+template <class WT>
+struct RowsMode<PQKV<WT>> {
+	static constexpr bool value = true;
+};
+
 template <class WT, class P, bool NORM, int THREADS, int U>
 static int launch_rb_t(const P &p, const float *x, const float *normw, float eps, int wpc, hipStream_t st) {
-	auto kern = gemv_rb_kernel<WT, P, U, NORM, THREADS>;
 	const int nb = std::max(1, std::min(p.n_groups, device_cu_count() * std::max(1, wpc)));
 	const int ngl = (p.n_groups + nb - 1) / nb;
+	if constexpr (RowsMode<P>::value) {
+		// every workgroup the same number of rows and a whole number of rows, at least 2,
+		// per wave (profiles/r3_gemv_rows.txt: W1|W3 fp16 39.4-40.0 -> 36.9 us, fp8 W2 13.4 ->
+		// 12.7-13.0; fp16 W2 with ONE 28-KB row per wave went 20.3 -> 21.3, so it keeps the
+		// chunk order); YALM_GEMV_ROWS=0 keeps the chunk order everywhere (A/B)
+		const bool rows_on = !getenv("YALM_GEMV_ROWS") || atoi(getenv("YALM_GEMV_ROWS")) != 0;
+		constexpr int W = THREADS / YALM_WAVE;
+		if (rows_on && p.n_groups % nb == 0 && (ngl * P::R) % W == 0 && ngl * P::R >= 2 * W) {
+			auto kern = gemv_rb_kernel<WT, P, U, NORM, THREADS, true>;
+			const size_t lds =
+			    ((size_t)((p.n + 3) & ~3) + 64 + (size_t)ngl * P::R * (THREADS / YALM_WAVE)) * sizeof(float);
+			if (lds > 65536)
+				HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+			hipLaunchKernelGGL(kern, dim3(nb), dim3(THREADS), lds, st, p, x, normw, eps);
+			HIPCHK(hipGetLastError());
+			return YALM_OK;
+		}
+	}
+	auto kern = gemv_rb_kernel<WT, P, U, NORM, THREADS>;
 	const size_t lds = ((size_t)((p.n + 3) & ~3) + 64 + (size_t)ngl * P::R * (THREADS / YALM_WAVE)) * sizeof(float);
 	if (lds > 65536)
 		HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
