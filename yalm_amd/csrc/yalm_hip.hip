@@ -186,15 +186,18 @@ static GemvCfg default_rb_cfg(int kind) {
 		switch (kind) {
 		case GK_W2:
 			return GemvCfg{512, 4, 1};
-		case GK_GLU: // round-2 resweep (profiles/r2_sweep_rb_fp8.txt): 21.4 us vs 22.5 for {1024, 2, 2}
-			return GemvCfg{512, 2, 2};
+		case GK_GLU: // round 3, whole-row mode (14 rows per wave): 20.5 us vs 21.4-21.6 for {512, 2, 2}
+			return GemvCfg{512, 4, 1};
+		case GK_QKV: // round 3, whole-row mode (3 rows per wave): 7.6 us vs 8.0-8.4 for {512, 2, 2}
+			return GemvCfg{512, 4, 1};
 		default:
 			return GemvCfg{512, 2, 2};
 		}
 	}
 	switch (kind) {
-	case GK_QKV:
-		return GemvCfg{512, 2, 2};
+	case GK_QKV: // one workgroup per CU: 24 rows each = 3 whole rows per wave (ROWS mode),
+	             // 10.6-10.7 vs 11.2-11.4 us for {512, 2, 2} (profiles/r3_gemv_rows.txt)
+		return GemvCfg{512, 4, 1};
 	case GK_WO:
 		return GemvCfg{1024, 2, 2};
 	case GK_W2:
