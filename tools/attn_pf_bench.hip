@@ -200,6 +200,14 @@ static void launch_v1(const uint16_t *Q, const uint16_t *kc, const uint16_t *vc,
 	pf::attn_prefill_kernel<128><<<grid, pf::THREADS, pf::attn_prefill_lds<128>(), st>>>(Q, kc, vc, T, pos0, nh, nkv, O);
 }
 
+// 32-key tiles: half the LDS per workgroup (32 KB) and fewer registers, so 3 workgroups per CU
+static void launch_v2(const uint16_t *Q, const uint16_t *kc, const uint16_t *vc, int T, int pos0, int nh, int nkv,
+                      uint16_t *O, hipStream_t st) {
+	const dim3 grid(nh, (T + pf::AQ - 1) / pf::AQ);
+	pf::attn_prefill_kernel<128, 32><<<grid, pf::THREADS, pf::attn_prefill_lds<128, 32>(), st>>>(Q, kc, vc, T, pos0, nh,
+	                                                                                          nkv, O);
+}
+
 int main(int argc, char **argv) {
 	const int T = argc > 1 ? atoi(argv[1]) : 4096;
 	const int rounds = argc > 2 ? atoi(argv[2]) : 5;
@@ -226,7 +234,9 @@ int main(int argc, char **argv) {
 	                       (int)pf::attn_prefill_lds<128>()));
 	CK(hipFuncSetAttribute((const void *)pf::attn_prefill_kernel_r3<128>, hipFuncAttributeMaxDynamicSharedMemorySize,
 	                       (int)pf::attn_prefill_lds<128>()));
-	std::vector<Variant> vs = {{"r3", launch_v0}, {"product", launch_v1}};
+	CK(hipFuncSetAttribute((const void *)pf::attn_prefill_kernel<128, 32>, hipFuncAttributeMaxDynamicSharedMemorySize,
+	                       (int)pf::attn_prefill_lds<128, 32>()));
+	std::vector<Variant> vs = {{"r3", launch_v0}, {"product", launch_v1}, {"kt32", launch_v2}};
 	const int nv = (int)vs.size();
 	std::vector<uint16_t *> outs(nv);
 	for (auto &o : outs)

@@ -403,22 +403,22 @@ __global__ __launch_bounds__(THREADS) void gemm_nt_kernel(const uint16_t *__rest
 //   its B fragments are row reads)
 constexpr int AQ = 128, AKT = 64; // queries per workgroup, keys per tile
 
-// Dynamic LDS of attn_prefill_kernel<D>: K[2][AKT][D], V[2][AKT][D] (f16).
-template <int D>
+// Dynamic LDS of attn_prefill_kernel<D, KT>: K[2][KT][D], V[2][KT][D] (f16).
+template <int D, int KT = AKT>
 constexpr size_t attn_prefill_lds() {
-	return (size_t)(4 * AKT * D) * 2;
+	return (size_t)(4 * KT * D) * 2;
 }
 
 // Stage one 64-key tile of K or V (rows key0.., kv head g) by LDS-DMA. Row r of
 // the lane-linear image holds source chunk c ^ sw(r): sw = r % (D/8) for K
 // (row reads of 16 B, conflict-spread over 16 rows) and (r & 3) << 1 for V
 // (ds_read_b64_tr_b16 reads 4 rows x 32 B: the 4 rows land on distinct banks).
-template <int D, bool ISV>
+template <int D, bool ISV, int KT = AKT>
 __device__ __forceinline__ void stage_kv(uint16_t *dst, const uint16_t *__restrict__ src, int key0, int kv_rows,
                                          int kv_dim, int g, int wave, int lane) {
 	constexpr int DCH = D / 8;
 	constexpr int RPI = 1024 / (D * 2); // rows per 1-KB wave-instruction
-	constexpr int NI = AKT / RPI / 4;   // instructions per wave
+	constexpr int NI = KT / RPI / 4;    // instructions per wave
 #pragma unroll
 	for (int i = 0; i < NI; ++i) {
 		const int rb = wave * NI + i;
@@ -441,16 +441,18 @@ typedef short short4_t __attribute__((ext_vector_type(4)));
 // 16 s + 8 (e >> 2) + 4 h + (e & 3) of the 32-key block) with V^T fragments
 // from hardware-transposed LDS reads. O^T keeps the query on the lane too, so
 // the online-softmax rescale is one per-lane factor.
-template <int D>
+template <int D, int KT = AKT>
 __global__ __launch_bounds__(THREADS) void attn_prefill_kernel(const uint16_t *__restrict__ Q,
                                                                const uint16_t *__restrict__ kc,
                                                                const uint16_t *__restrict__ vc, int T, int pos0,
                                                                int n_heads, int n_kv, uint16_t *__restrict__ O) {
 	static_assert(D == 64 || D == 128, "head_dim");
+	static_assert(KT == 32 || KT == 64, "keys per tile");
+	constexpr int NJ = KT / 32; // 32-key blocks per tile
 	constexpr int DCH = D / 8;
 	extern __shared__ __attribute__((aligned(16))) uint16_t asmem[];
-	uint16_t *const Kb = asmem;               // [2][AKT * D]
-	uint16_t *const Vb = asmem + 2 * AKT * D; // [2][AKT * D]
+	uint16_t *const Kb = asmem;               // [2][KT * D]
+	uint16_t *const Vb = asmem + 2 * KT * D; // [2][KT * D]
 	const int lane = threadIdx.x & 63, l32 = lane & 31, hh = lane >> 5;
 	const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 	// grid (heads, query blocks), x fastest: every head's heaviest (latest) query block
@@ -478,34 +480,34 @@ __global__ __launch_bounds__(THREADS) void attn_prefill_kernel(const uint16_t *_
 		o[jd] = f32x16_t{};
 	float m = -FLT_MAX, l = 0.0f;
 	const int qmax_blk = min(qb * AQ + AQ, T) - 1; // last query row of the block
-	const int ntile = (pos0 + qmax_blk) / AKT + 1; // key tiles up to its position
+	const int ntile = (pos0 + qmax_blk) / KT + 1; // key tiles up to its position
 	// transposed-read lane geometry (ds_read_b64_tr_b16: 16-lane groups, 4 rows x 16 columns)
 	const int gi = lane & 15, gq = gi >> 2, gp = gi & 3;
 	const int dgrp = 16 * ((lane >> 4) & 1);
 
-	stage_kv<D, false>(Kb, kc, 0, kv_rows, kv_dim, g, wave, lane);
-	stage_kv<D, true>(Vb, vc, 0, kv_rows, kv_dim, g, wave, lane);
+	stage_kv<D, false, KT>(Kb, kc, 0, kv_rows, kv_dim, g, wave, lane);
+	stage_kv<D, true, KT>(Vb, vc, 0, kv_rows, kv_dim, g, wave, lane);
 	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 	__syncthreads();
 	int cur = 0;
 	for (int kt = 0; kt < ntile; ++kt) {
-		const int key0 = kt * AKT;
+		const int key0 = kt * KT;
 		if (kt + 1 < ntile) { // next tile's LDS-DMA overlaps this tile's math
-			stage_kv<D, false>(Kb + (cur ^ 1) * AKT * D, kc, key0 + AKT, kv_rows, kv_dim, g, wave, lane);
-			stage_kv<D, true>(Vb + (cur ^ 1) * AKT * D, vc, key0 + AKT, kv_rows, kv_dim, g, wave, lane);
+			stage_kv<D, false, KT>(Kb + (cur ^ 1) * KT * D, kc, key0 + KT, kv_rows, kv_dim, g, wave, lane);
+			stage_kv<D, true, KT>(Vb + (cur ^ 1) * KT * D, vc, key0 + KT, kv_rows, kv_dim, g, wave, lane);
 		}
-		const uint16_t *Ks = Kb + cur * AKT * D;
-		const uint16_t *Vs = Vb + cur * AKT * D;
+		const uint16_t *Ks = Kb + cur * KT * D;
+		const uint16_t *Vs = Vb + cur * KT * D;
 
 		// a tile wholly past this wave's last query (the block's second diagonal tile for
 		// its first waves) adds nothing: skip its math (the wave still stages and syncs)
 		const bool live = key0 <= pos0 + qw0 + 31;
 		// ---- S^T = K Q^T: two 32-key blocks; register r of block j is key key0 + 32 j + crow(r, lane)
-		f32x16_t st[2];
-		half8_t pb[2][2]; // P^T fragments: [block j][k-step s]
+		f32x16_t st[NJ];
+		half8_t pb[NJ][2]; // P^T fragments: [block j][k-step s]
 		if (live) {
 #pragma unroll
-			for (int j = 0; j < 2; ++j) {
+			for (int j = 0; j < NJ; ++j) {
 				st[j] = f32x16_t{};
 				const int kr = 32 * j + l32;
 #pragma unroll
@@ -518,9 +520,9 @@ __global__ __launch_bounds__(THREADS) void attn_prefill_kernel(const uint16_t *_
 			// ---- online softmax for this lane's query. Raw scores; the 1/sqrt(D) log2(e)
 			// scale is folded into the exponent's FMA (sl2 > 0: the max commutes with it).
 			// Causal mask only on diagonal tiles (a uniform branch).
-			if (key0 + AKT - 1 > pos0 + qw0) {
+			if (key0 + KT - 1 > pos0 + qw0) {
 #pragma unroll
-				for (int j = 0; j < 2; ++j)
+				for (int j = 0; j < NJ; ++j)
 #pragma unroll
 					for (int r = 0; r < 16; ++r)
 						if (key0 + 32 * j + crow(r, lane) > qpos)
@@ -528,11 +530,11 @@ __global__ __launch_bounds__(THREADS) void attn_prefill_kernel(const uint16_t *_
 			}
 			float mx = st[0][0];
 #pragma unroll
-			for (int j = 0; j < 2; ++j)
+			for (int j = 0; j < NJ; ++j)
 #pragma unroll
 				for (int r = (j == 0 ? 1 : 0); r < 16; ++r)
 					mx = fmaxf(mx, st[j][r]);
-			mx = fmaxf(mx, xor32(mx)) * sl2; // the other lane half holds the other 32 keys
+			mx = fmaxf(mx, xor32(mx)) * sl2; // the other lane half holds the other keys of each block
 			// deferred rescale (cdna_hip_programming.md T13): while no query's max grows by
 			// more than 2^RESCALE_LOG2 the old max stays the reference (P <= 2^8, exact
 			// enough in f16; l and O are f32); otherwise every lane moves to its new max.
@@ -548,7 +550,7 @@ __global__ __launch_bounds__(THREADS) void attn_prefill_kernel(const uint16_t *_
 			}
 			float ls = 0.0f;
 #pragma unroll
-			for (int j = 0; j < 2; ++j)
+			for (int j = 0; j < NJ; ++j)
 #pragma unroll
 				for (int r = 0; r < 16; ++r) {
 					const float p = __builtin_amdgcn_exp2f(fmaf(st[j][r], sl2, -m));
@@ -561,7 +563,7 @@ __global__ __launch_bounds__(THREADS) void attn_prefill_kernel(const uint16_t *_
 		// ---- O^T += V^T P^T
 		if (live) {
 #pragma unroll
-			for (int j = 0; j < 2; ++j)
+			for (int j = 0; j < NJ; ++j)
 #pragma unroll
 				for (int s = 0; s < 2; ++s) {
 					const int klo = 32 * j + 16 * s + 4 * hh + gq; // keys of elements 0..3 (row gq of the 4-row block)
