@@ -13,6 +13,10 @@ replay. Weights are random (no checkpoints offline) but of the real
 architecture and size, generated in HBM before timing. The prompt is 13
 synthetic token ids (the README prompt's length) hydrated first.
 
+At N = 1 fp16 the line also carries `prefill`: config 4 (Llama-3.2-3B, one
+4096-position `-m perplexity` pass as a batched MFMA prefill) with its own
+MFMA roofline (`--no-prefill` skips it).
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype fp16|fp8]
 With --gpus N > 1 and no WORLD_SIZE in the environment, the script starts N
 rank processes itself (before any GPU call); under torch.distributed.run each
@@ -49,6 +53,9 @@ def parse():
     ap.add_argument("--tp-transport", default="rccl", choices=["rccl", "ipc"],
                     help="all-reduce transport for tensor parallelism: RCCL (one rank per GPU) or the IPC one-shot exchange")
     ap.add_argument("--no-envelope", action="store_true")
+    ap.add_argument("--no-prefill", action="store_true",
+                    help="skip the config-4 leg (Llama-3.2-3B 4096-position batched prefill, N = 1 fp16 only)")
+    ap.add_argument("--prefill-iters", type=int, default=3)
     ap.add_argument("--no-alt", action="store_true",
                     help="N > 1 over RCCL: skip the second measurement through the IPC exchange")
     ap.add_argument("--no-gpu-state", action="store_true",
@@ -193,6 +200,64 @@ def cpu_baseline(cfg, budget_s):
                   f"same synthetic Mistral-7B {'fp16' if cfg.weight_dtype == 1 else 'fp8'} weights, "
                   f"{threads} OpenMP threads = the host CPUs this job may use (nproc {nproc}, "
                   f"cgroup quota {quota}, OMP_NUM_THREADS {share or 'unset'}), {el:.1f} s",
+    }
+
+
+MFMA_F16_PEAK_TFLOPS = 2500.0  # MI355X dense f16 (MI355X_MICROARCH.md; no sparsity)
+
+
+def prefill_leg(runtime, M, model="llama-3.2-3b", n=4096, iters=3, check=48):
+    """Config 4 (BASELINE.json): `-m perplexity` over an n-position context as ONE
+    batched MFMA prefill (yalm_prefill) instead of the reference's n - 1 sequential
+    forwards (main.cpp:128-200). Synthetic weights of the real shape, synthetic ids.
+    Time = HIP events around `iters` whole passes on the decoder stream (yalm_prefill_time),
+    flops = the GEMMs + causal attention + logits; a spot check of the first `check`
+    positions' log p against the decode engine (the oracle check at these dims is
+    tests/test_gpu_prefill_llama.py)."""
+    import numpy as np
+
+    cfg = M.PRESETS[model].with_(weight_dtype=M.F16, max_seq_len=max(n, 64))
+    q_dim, kv_dim = cfg.n_heads * cfg.head_dim, cfg.n_kv_heads * cfg.head_dim
+    gemm = 2 * n * (cfg.dim * (q_dim + 2 * kv_dim) + q_dim * cfg.dim + 3 * cfg.dim * cfg.hidden_dim)
+    attn = 4 * cfg.head_dim * cfg.n_heads * n * (n + 1) // 2
+    flops = cfg.n_layers * (gemm + attn) + 2 * n * cfg.dim * cfg.vocab_size
+    dm = runtime.DeviceModel.synthetic(cfg, seed=5)
+    dec = runtime.Decoder(dm)
+    dec2 = None
+    try:
+        ms = dec.prefill_time(n, iters)
+        tflops = flops / (ms * 1e-3) / 1e12
+        rng = np.random.default_rng(0)
+        tokens = rng.integers(0, cfg.vocab_size, size=check + 1).astype(np.int32)
+        lp_p = dec.prefill(tokens)
+        dec2 = runtime.Decoder(dm)
+        lp_d = []
+        t0 = time.perf_counter()
+        for pos in range(check):
+            lg = dec2.forward(int(tokens[pos]), pos).astype(np.float64)
+            m = lg.max()
+            lp_d.append(lg[tokens[pos + 1]] - m - np.log(np.exp(lg - m).sum()))
+        seq_s = (time.perf_counter() - t0) / check
+        err = float(np.max(np.abs(lp_p[:check] - np.array(lp_d))))
+    finally:
+        if dec2 is not None:
+            dec2.close()
+        dec.close()
+        dm.close()
+    return {
+        "metric": f"prefill ms {model} fp16 {n}-position perplexity pass",
+        "value": round(ms, 3),
+        "unit": "ms",
+        "higher_is_better": False,
+        "iters": iters,
+        "tok_per_s": round(n / (ms * 1e-3), 1),
+        "flops": flops,
+        "roofline": {"bound": "mfma", "achieved": round(tflops, 1), "peak": MFMA_F16_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(tflops / MFMA_F16_PEAK_TFLOPS, 4)},
+        "sequential_decode_ms_per_position": round(seq_s * 1e3, 3),
+        "speedup_vs_sequential": round(seq_s * n / (ms * 1e-3), 1),
+        "spot_check": {"positions": check, "max_abs_dlogp_vs_decode": err},
+        "data": "synthetic weights of the real Llama-3.2-3B shape, synthetic token ids",
     }
 
 
@@ -424,6 +489,11 @@ def main():
             dm.close()
         except Exception as e:  # report, never hide
             out["tp_ipc"] = {"error": str(e)[:200]}
+    if world == 1 and args.dtype == "fp16" and not args.no_prefill:
+        try:  # config 4 beside config 2 (the decoder above is closed: its HBM is free again)
+            out["prefill"] = prefill_leg(runtime, M, iters=args.prefill_iters)
+        except Exception as e:  # report, never hide
+            out["prefill"] = {"error": repr(e)[:300]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)

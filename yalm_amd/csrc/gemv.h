@@ -421,6 +421,102 @@ __global__ __launch_bounds__(GEMV_THREADS) void gemv_kernel(P p, const float *__
 	}
 }
 
+// Whole-row GEMV with x held in registers (round 3, gemv_rb_kernel with XR = NCH): the ROWS order
+// when a row is exactly NCH 1-KB chunks (n = NCH * 64 * EPL, NCH % U == 0: W1|W3 and
+// QKV at n 4096 for f16 (NCH 8) and fp8 (NCH 4)). Every lane touches the same
+// NCH * EPL elements of x in every row, so they are read from LDS once (64 VGPRs)
+// instead of once per row; the row loop is unrolled over its chunks, which makes the
+// refill slot (c % U) and the next item's position compile-time. Same per-lane FMA
+// order (one accumulator, chunks in order) and the same reduction as gemv_rb_kernel,
+// so results are bit-identical to it.
+template <class WT, class P, int U, bool NORM, int THREADS, int NCH>
+__device__ __forceinline__ void gemv_rx_body(P p, const float *__restrict__ x, const float *__restrict__ normw,
+                                             float eps, float *xs) {
+	static_assert(NCH % U == 0, "the refill slot must be compile-time");
+	constexpr int R = P::R;
+	constexpr int EPL = WT::EPL;
+	constexpr int CH = YALM_WAVE * EPL;
+	constexpr size_t CHB = (size_t)CH * WT::BYTES;
+	constexpr int W = THREADS / YALM_WAVE;
+	const int n = p.n; // == NCH * CH (checked by the launcher)
+	const int NB = gridDim.x;
+	const int b = blockIdx.x;
+	const int lane = threadIdx.x & 63;
+	const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	const int ngl = b < p.n_groups ? (p.n_groups - 1 - b) / NB + 1 : 0;
+	const int nr = ngl * R > wave ? (ngl * R - 1 - wave) / W + 1 : 0; // rows wave, wave + W, ...
+	float *part = xs + ((n + 3) & ~3) + 64;                            // [ngl * R][W]
+	const size_t lane_off = (size_t)lane * EPL * WT::BYTES;
+	const char *dummy = (const char *)x + lane * 16;
+	auto rowp = [&](int i) { // row i of this wave (virtual row wave + i * W)
+		const int vr = wave + i * W;
+		const int gl = vr / R, r = vr - gl * R;
+		return p.row(b + gl * NB, r) + lane_off;
+	};
+
+	const bool xregs = n <= 4 * xpre_n<NORM>() * THREADS;
+	XPre<NORM> xp;
+	if (xregs)
+		prefetch_x<NORM>(xp, x, normw, n);
+	const char *cur = nr > 0 ? rowp(0) : dummy;
+	u32x4_t buf[U];
+#pragma unroll
+	for (int u = 0; u < U; ++u)
+		buf[u] = load_nt16(nr > 0 ? cur + (size_t)u * CHB : dummy);
+	p.prologue();
+	for (int i = threadIdx.x; i < ngl * R * W; i += THREADS)
+		part[i] = 0.0f;
+	if (xregs)
+		stage_x_regs<NORM>(xs, xp, n, eps);
+	else
+		stage_x<NORM>(xs, x, normw, n, eps);
+	float xr[NCH][EPL];
+#pragma unroll
+	for (int c = 0; c < NCH; ++c)
+#pragma unroll
+		for (int e = 0; e < EPL; e += 4) {
+			const float4_t t = *(const float4_t *)(xs + c * CH + lane * EPL + e);
+			xr[c][e] = t[0];
+			xr[c][e + 1] = t[1];
+			xr[c][e + 2] = t[2];
+			xr[c][e + 3] = t[3];
+		}
+
+	for (int i = 0; i < nr; ++i) {
+		const char *next = i + 1 < nr ? rowp(i + 1) : dummy;
+		float acc = 0.0f;
+#pragma unroll
+		for (int c = 0; c < NCH; ++c) {
+			float wf[EPL];
+			WT::unpack(buf[c % U], wf);
+#pragma unroll
+			for (int e = 0; e < EPL; ++e)
+				acc = fmaf(wf[e], xr[c][e], acc);
+			// refill with item (i, c + U): this row's chunk c + U, or the next row's
+			const char *a = c + U < NCH ? cur + (size_t)(c + U) * CHB
+			                            : (next == dummy ? dummy : next + (size_t)(c + U - NCH) * CHB);
+			buf[c % U] = load_nt16(a);
+		}
+		const float s = wave_sum(acc);
+		if (lane == 0)
+			part[(wave + i * W) * W + wave] = s;
+		cur = next;
+	}
+	__syncthreads();
+	for (int gl = threadIdx.x; gl < ngl; gl += THREADS) {
+		float a[R];
+#pragma unroll
+		for (int r = 0; r < R; ++r) {
+			float t = 0.0f;
+#pragma unroll
+			for (int w = 0; w < W; ++w)
+				t += part[(gl * R + r) * W + w];
+			a[r] = t;
+		}
+		p.finish_all(b + gl * NB, a);
+	}
+}
+
 // Row-block GEMV — the production path (n % (64 * EPL) == 0).
 //
 // One workgroup per CU (gridDim.x = NB ~ CU count): row group g belongs to
@@ -443,10 +539,14 @@ __global__ __launch_bounds__(GEMV_THREADS) void gemv_kernel(P p, const float *__
 // chunks of its rows, so the wave reduction runs once per row instead of once per 1-KB
 // chunk (W1|W3 at n 4096: 8 reductions per row -> 1; tools/pattern_bench.hip: the chunk
 // order with its per-chunk work ran 10-25% below the streaming envelope, whole rows at it).
-template <class WT, class P, int U, bool NORM, int THREADS, bool ROWS = false>
+template <class WT, class P, int U, bool NORM, int THREADS, bool ROWS = false, int XR = 0>
 __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__restrict__ x,
                                                           const float *__restrict__ normw, float eps) {
 	extern __shared__ __attribute__((aligned(16))) float xs[];
+	if constexpr (XR > 0) { // whole rows of XR chunks, x in registers (gemv_rx_body)
+		gemv_rx_body<WT, P, U, NORM, THREADS, XR>(p, x, normw, eps, xs);
+		return;
+	}
 	constexpr int R = P::R;
 	constexpr int EPL = WT::EPL;
 	constexpr int CH = YALM_WAVE * EPL;
@@ -556,3 +656,4 @@ __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__re
 	}
 #endif
 }
+
