@@ -266,22 +266,25 @@ __device__ __forceinline__ void stage_x(float *xs, const float *__restrict__ x, 
 
 // x (and the norm weights) loaded into registers BEFORE the weight stream is
 // issued, so the staging does not wait behind the weight loads (vmcnt is in
-// order): XPRE<NORM> float4 per thread (2 with the norm weights, 4 without:
-// n <= 4 * XPRE * blockDim.x); finished by stage_x_regs.
-template <bool NORM>
+// order): xpre_n float4 per thread (2 with the norm weights, 4 without:
+// n <= 4 * xpre_n * blockDim.x); finished by stage_x_regs.
+// Without the norm at 512 threads: 7 float4 = n 14336 (W2's hb for Mistral; round 3: the fp8
+// W2 at {512, 4, 1} staged its 57 KB x from global AFTER its first weight loads, so the first
+// FMA waited for both round trips in vmcnt order).
+template <bool NORM, int THREADS>
 constexpr int xpre_n() {
-	return NORM ? 2 : 4;
+	return NORM ? 2 : (THREADS == 512 ? 7 : 4);
 }
-template <bool NORM>
+template <bool NORM, int THREADS>
 struct XPre {
-	float4_t x[xpre_n<NORM>()], w[NORM ? xpre_n<NORM>() : 1];
+	float4_t x[xpre_n<NORM, THREADS>()], w[NORM ? xpre_n<NORM, THREADS>() : 1];
 };
-template <bool NORM>
-__device__ __forceinline__ void prefetch_x(XPre<NORM> &r, const float *__restrict__ x, const float *__restrict__ normw,
-                                           int n) {
+template <bool NORM, int THREADS>
+__device__ __forceinline__ void prefetch_x(XPre<NORM, THREADS> &r, const float *__restrict__ x,
+                                           const float *__restrict__ normw, int n) {
 	const int nthreads = blockDim.x;
 #pragma unroll
-	for (int k = 0; k < xpre_n<NORM>(); ++k) {
+	for (int k = 0; k < xpre_n<NORM, THREADS>(); ++k) {
 		int i = (threadIdx.x + k * nthreads) * 4;
 		i = i < n ? i : n - 4; // unconditional (clamped) loads: no branch for hipcc to wait at
 		r.x[k] = *(const float4_t *)(x + i);
@@ -290,8 +293,8 @@ __device__ __forceinline__ void prefetch_x(XPre<NORM> &r, const float *__restric
 	}
 }
 // infer.cpp:134-144 statement order, as stage_x
-template <bool NORM>
-__device__ __forceinline__ void stage_x_regs(float *xs, const XPre<NORM> &r, int n, float eps) {
+template <bool NORM, int THREADS>
+__device__ __forceinline__ void stage_x_regs(float *xs, const XPre<NORM, THREADS> &r, int n, float eps) {
 	const int tid = threadIdx.x;
 	const int nthreads = blockDim.x;
 	float scale = 1.0f;
@@ -299,7 +302,7 @@ __device__ __forceinline__ void stage_x_regs(float *xs, const XPre<NORM> &r, int
 		float *red = xs + ((n + 3) & ~3);
 		float ss = 0.0f;
 #pragma unroll
-		for (int k = 0; k < xpre_n<NORM>(); ++k) {
+		for (int k = 0; k < xpre_n<NORM, THREADS>(); ++k) {
 			if ((tid + k * nthreads) * 4 < n) {
 				const float4_t v = r.x[k];
 				ss += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
@@ -316,7 +319,7 @@ __device__ __forceinline__ void stage_x_regs(float *xs, const XPre<NORM> &r, int
 		scale = 1.0f / rms;
 	}
 #pragma unroll
-	for (int k = 0; k < xpre_n<NORM>(); ++k) {
+	for (int k = 0; k < xpre_n<NORM, THREADS>(); ++k) {
 		const int i = (tid + k * nthreads) * 4;
 		if (i < n) {
 			float4_t v = r.x[k];
@@ -421,102 +424,6 @@ __global__ __launch_bounds__(GEMV_THREADS) void gemv_kernel(P p, const float *__
 	}
 }
 
-// Whole-row GEMV with x held in registers (round 3, gemv_rb_kernel with XR = NCH): the ROWS order
-// when a row is exactly NCH 1-KB chunks (n = NCH * 64 * EPL, NCH % U == 0: W1|W3 and
-// QKV at n 4096 for f16 (NCH 8) and fp8 (NCH 4)). Every lane touches the same
-// NCH * EPL elements of x in every row, so they are read from LDS once (64 VGPRs)
-// instead of once per row; the row loop is unrolled over its chunks, which makes the
-// refill slot (c % U) and the next item's position compile-time. Same per-lane FMA
-// order (one accumulator, chunks in order) and the same reduction as gemv_rb_kernel,
-// so results are bit-identical to it.
-template <class WT, class P, int U, bool NORM, int THREADS, int NCH>
-__device__ __forceinline__ void gemv_rx_body(P p, const float *__restrict__ x, const float *__restrict__ normw,
-                                             float eps, float *xs) {
-	static_assert(NCH % U == 0, "the refill slot must be compile-time");
-	constexpr int R = P::R;
-	constexpr int EPL = WT::EPL;
-	constexpr int CH = YALM_WAVE * EPL;
-	constexpr size_t CHB = (size_t)CH * WT::BYTES;
-	constexpr int W = THREADS / YALM_WAVE;
-	const int n = p.n; // == NCH * CH (checked by the launcher)
-	const int NB = gridDim.x;
-	const int b = blockIdx.x;
-	const int lane = threadIdx.x & 63;
-	const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-	const int ngl = b < p.n_groups ? (p.n_groups - 1 - b) / NB + 1 : 0;
-	const int nr = ngl * R > wave ? (ngl * R - 1 - wave) / W + 1 : 0; // rows wave, wave + W, ...
-	float *part = xs + ((n + 3) & ~3) + 64;                            // [ngl * R][W]
-	const size_t lane_off = (size_t)lane * EPL * WT::BYTES;
-	const char *dummy = (const char *)x + lane * 16;
-	auto rowp = [&](int i) { // row i of this wave (virtual row wave + i * W)
-		const int vr = wave + i * W;
-		const int gl = vr / R, r = vr - gl * R;
-		return p.row(b + gl * NB, r) + lane_off;
-	};
-
-	const bool xregs = n <= 4 * xpre_n<NORM>() * THREADS;
-	XPre<NORM> xp;
-	if (xregs)
-		prefetch_x<NORM>(xp, x, normw, n);
-	const char *cur = nr > 0 ? rowp(0) : dummy;
-	u32x4_t buf[U];
-#pragma unroll
-	for (int u = 0; u < U; ++u)
-		buf[u] = load_nt16(nr > 0 ? cur + (size_t)u * CHB : dummy);
-	p.prologue();
-	for (int i = threadIdx.x; i < ngl * R * W; i += THREADS)
-		part[i] = 0.0f;
-	if (xregs)
-		stage_x_regs<NORM>(xs, xp, n, eps);
-	else
-		stage_x<NORM>(xs, x, normw, n, eps);
-	float xr[NCH][EPL];
-#pragma unroll
-	for (int c = 0; c < NCH; ++c)
-#pragma unroll
-		for (int e = 0; e < EPL; e += 4) {
-			const float4_t t = *(const float4_t *)(xs + c * CH + lane * EPL + e);
-			xr[c][e] = t[0];
-			xr[c][e + 1] = t[1];
-			xr[c][e + 2] = t[2];
-			xr[c][e + 3] = t[3];
-		}
-
-	for (int i = 0; i < nr; ++i) {
-		const char *next = i + 1 < nr ? rowp(i + 1) : dummy;
-		float acc = 0.0f;
-#pragma unroll
-		for (int c = 0; c < NCH; ++c) {
-			float wf[EPL];
-			WT::unpack(buf[c % U], wf);
-#pragma unroll
-			for (int e = 0; e < EPL; ++e)
-				acc = fmaf(wf[e], xr[c][e], acc);
-			// refill with item (i, c + U): this row's chunk c + U, or the next row's
-			const char *a = c + U < NCH ? cur + (size_t)(c + U) * CHB
-			                            : (next == dummy ? dummy : next + (size_t)(c + U - NCH) * CHB);
-			buf[c % U] = load_nt16(a);
-		}
-		const float s = wave_sum(acc);
-		if (lane == 0)
-			part[(wave + i * W) * W + wave] = s;
-		cur = next;
-	}
-	__syncthreads();
-	for (int gl = threadIdx.x; gl < ngl; gl += THREADS) {
-		float a[R];
-#pragma unroll
-		for (int r = 0; r < R; ++r) {
-			float t = 0.0f;
-#pragma unroll
-			for (int w = 0; w < W; ++w)
-				t += part[(gl * R + r) * W + w];
-			a[r] = t;
-		}
-		p.finish_all(b + gl * NB, a);
-	}
-}
-
 // Row-block GEMV — the production path (n % (64 * EPL) == 0).
 //
 // One workgroup per CU (gridDim.x = NB ~ CU count): row group g belongs to
@@ -539,14 +446,10 @@ __device__ __forceinline__ void gemv_rx_body(P p, const float *__restrict__ x, c
 // chunks of its rows, so the wave reduction runs once per row instead of once per 1-KB
 // chunk (W1|W3 at n 4096: 8 reductions per row -> 1; tools/pattern_bench.hip: the chunk
 // order with its per-chunk work ran 10-25% below the streaming envelope, whole rows at it).
-template <class WT, class P, int U, bool NORM, int THREADS, bool ROWS = false, int XR = 0>
+template <class WT, class P, int U, bool NORM, int THREADS, bool ROWS = false>
 __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__restrict__ x,
                                                           const float *__restrict__ normw, float eps) {
 	extern __shared__ __attribute__((aligned(16))) float xs[];
-	if constexpr (XR > 0) { // whole rows of XR chunks, x in registers (gemv_rx_body)
-		gemv_rx_body<WT, P, U, NORM, THREADS, XR>(p, x, normw, eps, xs);
-		return;
-	}
 	constexpr int R = P::R;
 	constexpr int EPL = WT::EPL;
 	constexpr int CH = YALM_WAVE * EPL;
@@ -591,10 +494,10 @@ __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__re
 
 	int ivr = ROWS ? wave : wave / nch, ic = ROWS ? 0 : wave - (wave / nch) * nch; // issue cursor
 	const int vr0 = ivr, c0 = ic;
-	const bool xregs = n <= 4 * xpre_n<NORM>() * THREADS; // x (+ norm weights) fit the registers
-	XPre<NORM> xp;
+	const bool xregs = n <= 4 * xpre_n<NORM, THREADS>() * THREADS; // x (+ norm weights) fit the registers
+	XPre<NORM, THREADS> xp;
 	if (xregs)
-		prefetch_x<NORM>(xp, x, normw, n); // ahead of the weight stream in vmcnt order
+		prefetch_x<NORM, THREADS>(xp, x, normw, n); // ahead of the weight stream in vmcnt order
 	u32x4_t buf[U];
 #pragma unroll
 	for (int u = 0; u < U; ++u) {
@@ -605,7 +508,7 @@ __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__re
 	for (int i = threadIdx.x; i < ngl * R * W; i += THREADS)
 		part[i] = 0.0f;
 	if (xregs)
-		stage_x_regs<NORM>(xs, xp, n, eps);
+		stage_x_regs<NORM, THREADS>(xs, xp, n, eps);
 	else
 		stage_x<NORM>(xs, x, normw, n, eps);
 

@@ -160,14 +160,6 @@ static int launch_rb_t(const P &p, const float *x, const float *normw, float eps
 		constexpr int W = THREADS / YALM_WAVE;
 		if (rows_on && p.n_groups % nb == 0 && (ngl * P::R) % W == 0 && ngl * P::R >= 2 * W) {
 			auto kern = gemv_rb_kernel<WT, P, U, NORM, THREADS, true>;
-			// rows of exactly 8 (f16) / 4 (fp8) 1-KB chunks: x in registers (gemv.h gemv_rx_body);
-			// YALM_GEMV_XREG=0 keeps it in LDS (A/B)
-			static const bool xreg_on = !getenv("YALM_GEMV_XREG") || atoi(getenv("YALM_GEMV_XREG")) != 0;
-			constexpr int CH = YALM_WAVE * WT::EPL;
-			constexpr int NCHX = WT::BYTES == 1 ? 4 : 8;
-			if constexpr (NCHX % U == 0 && WT::BYTES <= 2)
-				if (xreg_on && p.n == NCHX * CH)
-					kern = gemv_rb_kernel<WT, P, U, NORM, THREADS, true, NCHX>;
 			const size_t lds =
 			    ((size_t)((p.n + 3) & ~3) + 64 + (size_t)ngl * P::R * (THREADS / YALM_WAVE)) * sizeof(float);
 			if (lds > 65536)
