@@ -192,3 +192,18 @@ def test_prefill_matches_decode(name, n):
     dec_p.close()
     dec_d.close()
     dm.close()
+
+
+def test_bench_prefill_leg():
+    """bench.py's config-4 leg (the `prefill` object of the default line) on a small
+    model: the fields the driver reads, a finite MFMA rate, and its spot check of the
+    prefill's log p against the decode engine within LP_ATOL."""
+    import bench
+
+    R = rt()
+    out = bench.prefill_leg(R, M, model="small", n=200, iters=1, check=8)
+    assert out["unit"] == "ms" and out["value"] > 0 and out["higher_is_better"] is False
+    rl = out["roofline"]
+    assert rl["bound"] == "mfma" and 0 < rl["achieved"] and 0 < rl["frac"] < 1
+    assert out["flops"] > 0 and out["tok_per_s"] > 0
+    assert out["spot_check"]["max_abs_dlogp_vs_decode"] <= LP_ATOL
