@@ -13,9 +13,10 @@ replay. Weights are random (no checkpoints offline) but of the real
 architecture and size, generated in HBM before timing. The prompt is 13
 synthetic token ids (the README prompt's length) hydrated first.
 
-At N = 1 fp16 the line also carries `prefill`: config 4 (Llama-3.2-3B, one
-4096-position `-m perplexity` pass as a batched MFMA prefill) with its own
-MFMA roofline (`--no-prefill` skips it).
+At N = 1 fp16 the line also carries `fp8`: config 3, the same decode with E5M2
+weights (a child run of this script; `--no-fp8` skips it), and `prefill`:
+config 4 (Llama-3.2-3B, one 4096-position `-m perplexity` pass as a batched
+MFMA prefill) with its own MFMA roofline (`--no-prefill` skips it).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype fp16|fp8]
 With --gpus N > 1 and no WORLD_SIZE in the environment, the script starts N
@@ -56,6 +57,8 @@ def parse():
     ap.add_argument("--no-prefill", action="store_true",
                     help="skip the config-4 leg (Llama-3.2-3B 4096-position batched prefill, N = 1 fp16 only)")
     ap.add_argument("--prefill-iters", type=int, default=3)
+    ap.add_argument("--no-fp8", action="store_true",
+                    help="skip the config-3 leg (the same decode with E5M2 weights, N = 1 fp16 runs only)")
     ap.add_argument("--no-alt", action="store_true",
                     help="N > 1 over RCCL: skip the second measurement through the IPC exchange")
     ap.add_argument("--no-gpu-state", action="store_true",
@@ -294,6 +297,25 @@ def make_decoder(runtime, M, cfg, rank, world, mode, dist):
     return dm, runtime.Decoder(dm, tp_id=uid[0])
 
 
+def fp8_leg(args):
+    """Config 3 beside config 2: the same decode with fp8 (E5M2) weights, as a child run of
+    this script whose JSON line is parsed. Started BEFORE this process makes any GPU call (a
+    child of a process holding the GPU is not started here)."""
+    try:
+        cmd = [sys.executable, os.path.abspath(__file__), "--dtype", "fp8", "--steps", str(args.steps),
+               "--warmup", str(args.warmup), "--no-cpu-baseline", "--no-prefill", "--no-gpu-state",
+               "--kernel-iters", str(args.kernel_iters)] + (["--no-envelope"] if args.no_envelope else [])
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        if r.returncode != 0 or not lines:
+            raise RuntimeError(f"rc {r.returncode}: {(r.stderr or r.stdout)[-300:]}")
+        d8 = json.loads(lines[-1])
+        return {k: d8[k] for k in ("metric", "value", "unit", "ms_per_step", "dtype", "config", "step_roofline",
+                                   "roofline") if k in d8}
+    except Exception as e:  # report, never hide
+        return {"error": repr(e)[:300]}
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -311,6 +333,9 @@ def main():
         dist = dist_mod
 
     profiled = any(k.startswith("ROCPROF") for k in os.environ)
+    fp8_leg_out = None
+    if world == 1 and args.dtype == "fp16" and not args.no_fp8 and not profiled:
+        fp8_leg_out = fp8_leg(args)  # before any GPU call of this process
     state = gpu_state() if local_rank == 0 and not (args.no_gpu_state or profiled) else None
     from yalm_amd import models as M
     from yalm_amd import runtime
@@ -489,6 +514,8 @@ def main():
             dm.close()
         except Exception as e:  # report, never hide
             out["tp_ipc"] = {"error": str(e)[:200]}
+    if fp8_leg_out is not None:
+        out["fp8"] = fp8_leg_out
     if world == 1 and args.dtype == "fp16" and not args.no_prefill:
         try:  # config 4 beside config 2 (the decoder above is closed: its HBM is free again)
             out["prefill"] = prefill_leg(runtime, M, iters=args.prefill_iters)

@@ -8,7 +8,7 @@ for rep in 1 2; do
   for setting in "$@"; do
     k1=$(env $setting timeout -k 5 60 python tools/kernel_times.py --iters 256 --ctx 16 --dtype $dt | awk '/attn\+Wo gran/{a=$4} / Wo /{w=$3} END{print a" (Wo "w")"}')
     k2=$(env $setting timeout -k 5 60 python tools/kernel_times.py --iters 256 --ctx 150 --dtype $dt | awk '/attn\+Wo gran/{a=$4} / Wo /{w=$3} END{print a" (Wo "w")"}')
-    v=$(env $setting timeout -k 5 120 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-envelope --no-prefill --dtype $dt | python3 -c "import sys,json; d=json.loads(sys.stdin.readline()); print(d['value'])")
+    v=$(env $setting timeout -k 5 120 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-envelope --no-prefill --no-fp8 --dtype $dt | python3 -c "import sys,json; d=json.loads(sys.stdin.readline()); print(d['value'])")
     echo "$dt rep $rep [$setting]: attn+Wo kv17 $k1 us, kv151 $k2 us, bench(20) $v tok/s"
   done
 done

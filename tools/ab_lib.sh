@@ -13,7 +13,7 @@ for rep in 1 2; do
       done
     done
     for lib in $a $b; do
-      v=$(YALM_LIB=$lib timeout -k 5 120 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-envelope --no-prefill --dtype $dt | \
+      v=$(YALM_LIB=$lib timeout -k 5 120 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-envelope --no-prefill --no-fp8 --dtype $dt | \
           python3 -c "import sys,json; d=json.loads(sys.stdin.readline()); print(d['value'])")
       echo "rep $rep $dt bench(20) $(basename $lib): $v tok/s"
     done
