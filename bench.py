@@ -305,7 +305,7 @@ def fp8_leg(args):
         cmd = [sys.executable, os.path.abspath(__file__), "--dtype", "fp8", "--steps", str(args.steps),
                "--warmup", str(args.warmup), "--no-cpu-baseline", "--no-prefill", "--no-gpu-state",
                "--kernel-iters", str(args.kernel_iters)] + (["--no-envelope"] if args.no_envelope else [])
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
         lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
         if r.returncode != 0 or not lines:
             raise RuntimeError(f"rc {r.returncode}: {(r.stderr or r.stdout)[-300:]}")
