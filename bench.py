@@ -59,6 +59,11 @@ def parse():
     ap.add_argument("--prefill-iters", type=int, default=3)
     ap.add_argument("--no-fp8", action="store_true",
                     help="skip the config-3 leg (the same decode with E5M2 weights, N = 1 fp16 runs only)")
+    ap.add_argument("--no-long", action="store_true",
+                    help="skip the long-context leg (decode at the full 4096-slot window into the sink regime)")
+    ap.add_argument("--long-only", action="store_true",
+                    help="run only the long-context leg (N = 1 fp16; for profiling) and print its JSON")
+    ap.add_argument("--long-steps", type=int, default=64)
     ap.add_argument("--no-alt", action="store_true",
                     help="N > 1 over RCCL: skip the second measurement through the IPC exchange")
     ap.add_argument("--no-gpu-state", action="store_true",
@@ -264,6 +269,64 @@ def prefill_leg(runtime, M, model="llama-3.2-3b", n=4096, iters=3, check=48):
     }
 
 
+def long_context_leg(runtime, M, cfg, dm, steps=64, fill=4080, warmup=4, kernel_iters=64):
+    """Decode at the full 4096-slot window and into the StreamingLLM regime
+    (infer.cpp:483-485: kv_sink 2, ring slots, kv_len = max_seq_len; the README's
+    ~4800-token row, README.md:9-14). The cache is hydrated by one batched prefill
+    of `fill` synthetic positions (yalm_prefill, the CLI's prompt path), then
+    `steps` greedy tokens are timed from pos fill + 1 + warmup across
+    pos max_seq_len. Also times, at the final state (kv_len = max_seq_len), the
+    fused attention + Wo launch, the standalone split-KV attention and the plain
+    Wo GEMV (HIP events on the decoder stream, layers rotated)."""
+    import numpy as np
+
+    dec = runtime.Decoder(dm)
+    try:
+        rng = np.random.default_rng(1)
+        toks = rng.integers(3, cfg.vocab_size, size=fill).astype(np.int32)
+        dec.prefill(toks, 0, logprobs=False)
+        dec.generate_greedy(int(toks[-1]) % cfg.vocab_size, fill, 1)
+        if warmup:
+            dec.enqueue_greedy(warmup)
+        _, pos0 = dec.device_step()
+        t0 = time.perf_counter()
+        dec.enqueue_greedy(steps)
+        _, pos1 = dec.device_step()
+        el = time.perf_counter() - t0
+        kv = [M.kv_indices(cfg.max_seq_len, p)[2] for p in range(pos0, pos1)]
+        kv_avg = float(np.mean(kv))
+        bpt = cfg.weight_bytes_per_token() + cfg.kv_bytes_per_token(int(round(kv_avg)))
+        value = steps / el
+        kern = {}
+        for kid, key in ((8, "attn_wo_us"), (1, "attention_us"), (2, "wo_gemv_us")):
+            if kid == 8 and not dec.attn_wo:
+                continue
+            kern[key] = round(dec.time_kernel(kid, kernel_iters) * 1e3, 3)
+        kvb = cfg.kv_bytes_per_token(cfg.max_seq_len) // cfg.n_layers  # K + V bytes one layer's attention reads
+        wob = cfg.dim * cfg.q_dim * M.DTYPE_BYTES[cfg.weight_dtype]
+        if "attention_us" in kern:
+            kern["attention_kv_bytes"] = kvb
+            kern["attention_gbs"] = round(kvb / (kern["attention_us"] * 1e-6) / 1e9, 1)
+        if "attn_wo_us" in kern:
+            kern["attn_wo_bytes"] = kvb + wob
+            kern["attn_wo_gbs"] = round((kvb + wob) / (kern["attn_wo_us"] * 1e-6) / 1e9, 1)
+    finally:
+        dec.close()
+    return {
+        "metric": "decode tok/s Mistral-7B fp16 @1 GPU at the full 4096-slot window (sink regime)",
+        "value": round(value, 3),
+        "unit": "tok/s",
+        "steps": steps,
+        "ms_per_step": round(el / steps * 1e3, 4),
+        "pos": [int(pos0), int(pos1)],
+        "kv_len": [int(min(kv)), int(max(kv))],
+        "hydrate": f"batched prefill of {fill} synthetic positions, then {warmup + 1} greedy warm-up tokens",
+        "step_roofline": {"bytes_per_token": int(bpt), "achieved": round(bpt * value / 1e9, 1),
+                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(bpt * value / 1e9 / HBM_PEAK_GBS, 4)},
+        "kernels_at_kv_max": kern,
+    }
+
+
 def tp_bytes_per_token(cfg, size):
     """Algorithmic HBM bytes ONE rank reads per token under the Megatron split
     (include/yalm_hip.h): 1/size of every sharded matrix and of the classifier,
@@ -318,7 +381,14 @@ def fp8_leg(args):
 
 def main():
     args = parse()
+    if args.long_only:
+        args.no_fp8 = args.no_gpu_state = True
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        if any(k.startswith("ROCPROF") for k in os.environ):
+            # under rocprofv3 the profiler's preload has initialised the GPU in this process:
+            # starting rank processes from here would fork+exec a GPU-initialised process
+            sys.exit("bench.py --gpus N under a profiler: start the ranks with a launcher outside it "
+                     "(python -m torch.distributed.run ... bench.py) and put rocprofv3 on each rank's program")
         sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -370,6 +440,12 @@ def main():
         dm, dec = make_decoder(runtime, M, cfg, rank, world, mode, dist)
     tp = mode.startswith("tp-")
     tp_size = world if tp else 1
+    if args.long_only:
+        print(json.dumps(long_context_leg(runtime, M, cfg, dm, steps=args.long_steps,
+                                          kernel_iters=args.kernel_iters)), flush=True)
+        dec.close()
+        dm.close()
+        return
 
     def timed_decode(dec, tp):
         """Hydrate the prompt, warm up, then time exactly args.steps greedy tokens
@@ -401,11 +477,17 @@ def main():
         assert pos1 - pos0 == args.steps, (pos0, pos1)
         agree = None
         if dist is not None:
+            # every rank's whole greedy sequence since generate_greedy (first token, warm-up,
+            # timed steps), hashed: ranks that diverge and meet again still disagree
+            import hashlib
+
+            seq = dec.device_tokens()
+            h = hashlib.sha256(str(seq).encode()).hexdigest()
             allv = [None] * world
-            dist.all_gather_object(allv, (elapsed, tok1))
+            dist.all_gather_object(allv, (elapsed, h, len(seq)))
             elapsed = max(v[0] for v in allv)
             if tp:  # every rank must have produced the same token sequence
-                agree = len({v[1] for v in allv}) == 1
+                agree = len({(v[1], v[2]) for v in allv}) == 1
         return elapsed, pos0, pos1, agree
 
     elapsed, pos0, pos1, agree = timed_decode(dec, tp)
@@ -500,6 +582,12 @@ def main():
     if fallback:
         out["fallback"] = fallback
     dec.close()
+    if mode == "single" and args.dtype == "fp16" and not args.no_long:
+        try:  # decode at long context (kv_len 4096, sink regime) on the same weights
+            out["long_context"] = long_context_leg(runtime, M, cfg, dm, steps=args.long_steps,
+                                                   kernel_iters=args.kernel_iters)
+        except Exception as e:  # report, never hide
+            out["long_context"] = {"error": repr(e)[:300]}
     dm.close()
     if mode == "tp-rccl" and world > 1 and not args.no_alt:
         # the same workload through the IPC one-shot exchange (include/yalm_hip.h), for

@@ -125,6 +125,11 @@ int yalm_generate_greedy(yalm_decoder d, int token, int pos, int n_steps, int *o
 int yalm_enqueue_greedy(yalm_decoder d, int n_steps);
 /* Read back the device-resident next token / position after enqueue+sync. */
 int yalm_device_step(yalm_decoder d, int *token, int *pos);
+/* The greedy tokens produced on the device since the last yalm_generate_greedy
+ * (that call's tokens, then every yalm_enqueue_greedy step, up to 65536):
+ * copies min(*n_total, cap) of them to out (host) after a sync; *n_total = how many
+ * were produced. Lets tensor-parallel ranks compare whole sequences (bench.py). */
+int yalm_device_tokens(yalm_decoder d, int *out, int cap, int *n_total);
 /* Block::block (model.cpp:213-265) for one layer, eagerly, on the decoder's
  * current activation x (the test hook for per-layer parity). */
 int yalm_block(yalm_decoder d, int layer, int pos, int kv_sink, int kv_pos, int kv_len);

@@ -416,8 +416,17 @@ int awo_check(yalm_decoder_s *d) {
 		HIPCHK(hipMemcpy(&e, d->awo_err, sizeof(e), hipMemcpyDeviceToHost));
 		if (e) { // cleared so that later calls report only their own failures
 			HIPCHK(hipMemset(d->awo_err, 0, sizeof(e)));
-			set_err("fused attention + Wo launch gave up waiting for the attention heads (error bits " +
-			        std::to_string(e) + "); YALM_ATTN_WO=0 selects separate launches");
+			// bit 1: a Wo workgroup of the fused launch gave up waiting for its head granules;
+			// bit 2: a split-KV merger (fused or standalone attention) gave up waiting for a chunk
+			std::string m = "bounded in-launch wait gave up (results invalid):";
+			if (e & 1u)
+				m += " the fused attention + Wo launch's Wo gather timed out waiting for the attention heads"
+				     " (YALM_ATTN_WO=0 selects separate launches);";
+			if (e & 2u)
+				m += " the split-KV attention merger timed out waiting for a key-chunk partial;";
+			if (e & ~3u)
+				m += " unknown error bits " + std::to_string(e & ~3u) + ";";
+			set_err(m);
 			return YALM_ERR_HIP;
 		}
 	}
@@ -1087,6 +1096,19 @@ extern "C" int yalm_device_step(yalm_decoder d, int *token, int *pos) {
 	return YALM_OK;
 }
 
+extern "C" int yalm_device_tokens(yalm_decoder d, int *out, int cap, int *n_total) {
+	ARGCHK(d && n_total && cap >= 0 && (out || cap == 0), "yalm_device_tokens: bad argument");
+	StepState s;
+	HIPCHK(hipStreamSynchronize(d->stream));
+	TRY(awo_check(d));
+	HIPCHK(hipMemcpy(&s, d->step, sizeof(s), hipMemcpyDeviceToHost));
+	*n_total = s.n_gen;
+	const int n = std::min(std::min(s.n_gen, d->tokens_cap), cap);
+	if (n > 0)
+		HIPCHK(hipMemcpy(out, d->tokens, sizeof(int) * n, hipMemcpyDeviceToHost));
+	return YALM_OK;
+}
+
 extern "C" int yalm_block(yalm_decoder d, int layer, int pos, int kv_sink, int kv_pos, int kv_len) {
 	ARGCHK(d && layer >= 0 && layer < d->c.n_layers, "bad layer");
 	ARGCHK(kv_len >= 1 && kv_len <= d->c.max_seq_len && kv_pos >= 0 && kv_pos < d->c.max_seq_len,
@@ -1095,7 +1117,7 @@ extern "C" int yalm_block(yalm_decoder d, int layer, int pos, int kv_sink, int k
 	HIPCHK(hipGetLastError());
 	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_layer_t, d, layer));
 	HIPCHK(hipStreamSynchronize(d->stream));
-	return YALM_OK;
+	return awo_check(d);
 }
 
 extern "C" int yalm_get_x(yalm_decoder d, float *host) {

@@ -98,6 +98,7 @@ _sig("yalm_forward", c_int, [c_void_p, c_int, c_int, c_int, c_void_p])
 _sig("yalm_generate_greedy", c_int, [c_void_p, c_int, c_int, c_int, c_void_p])
 _sig("yalm_enqueue_greedy", c_int, [c_void_p, c_int])
 _sig("yalm_device_step", c_int, [c_void_p, ctypes.POINTER(c_int), ctypes.POINTER(c_int)])
+_sig("yalm_device_tokens", c_int, [c_void_p, c_void_p, c_int, ctypes.POINTER(c_int)])
 _sig("yalm_block", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int])
 _sig("yalm_get_x", c_int, [c_void_p, c_void_p])
 _sig("yalm_set_x", c_int, [c_void_p, c_void_p])
@@ -126,7 +127,7 @@ EXPORTED = [
     "yalm_last_error", "yalm_set_device", "yalm_upload", "yalm_alloc", "yalm_download", "yalm_register_host",
     "yalm_unregister_host", "yalm_free", "yalm_stream_create", "yalm_stream_destroy", "yalm_stream_sync",
     "yalm_synth", "yalm_decoder_create", "yalm_decoder_destroy", "yalm_forward", "yalm_generate_greedy",
-    "yalm_enqueue_greedy", "yalm_device_step", "yalm_block", "yalm_get_x", "yalm_set_x", "yalm_get_logits",
+    "yalm_enqueue_greedy", "yalm_device_step", "yalm_device_tokens", "yalm_block", "yalm_get_x", "yalm_set_x", "yalm_get_logits",
     "yalm_time_kernel", "yalm_kernel_name", "yalm_set_gemv_config", "yalm_matmul", "yalm_mha", "yalm_ffn",
     "yalm_prefill", "yalm_prefill_time", "yalm_gemm_f16", "yalm_attn_prefill", "yalm_tp_unique_id",
     "yalm_decoder_create_tp", "yalm_copy_2d", "yalm_tp_ipc_alloc", "yalm_decoder_create_tp_ipc",
@@ -419,6 +420,13 @@ class Decoder:
         t, p = c_int(), c_int()
         check(lib.yalm_device_step(self.h, ctypes.byref(t), ctypes.byref(p)))
         return t.value, p.value
+
+    def device_tokens(self, cap: int = 1 << 16) -> list:
+        """Greedy tokens produced on the device since the last generate_greedy."""
+        out = np.zeros(max(cap, 1), np.int32)
+        n = c_int()
+        check(lib.yalm_device_tokens(self.h, out.ctypes.data, cap, ctypes.byref(n)))
+        return out[:min(n.value, cap)].tolist()
 
     def block(self, layer, pos, kv_sink, kv_pos, kv_len):
         check(lib.yalm_block(self.h, layer, pos, kv_sink, kv_pos, kv_len))
