@@ -175,10 +175,7 @@ def cpu_baseline(cfg, budget_s):
 
     import oracle_py as O
 
-    nproc = len(os.sched_getaffinity(0))
-    quota = cgroup_cpus()
-    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)  # the harness's CPU share when no quota is readable
-    threads = min(nproc, quota or share or nproc)
+    threads, nproc, quota, share = cpu_threads()
     host = O.synth_host_tensors_fast(cfg, seed=1)
     om = O.OracleModel(cfg, host)
     prompt = [(7 * i + 1) % cfg.vocab_size for i in range(PROMPT_LEN)]
@@ -208,6 +205,71 @@ def cpu_baseline(cfg, budget_s):
                   f"same synthetic Mistral-7B {'fp16' if cfg.weight_dtype == 1 else 'fp8'} weights, "
                   f"{threads} OpenMP threads = the host CPUs this job may use (nproc {nproc}, "
                   f"cgroup quota {quota}, OMP_NUM_THREADS {share or 'unset'}), {el:.1f} s",
+    }
+
+
+def cpu_threads():
+    """(threads, nproc, cgroup quota, OMP_NUM_THREADS share) for the CPU baselines."""
+    nproc = len(os.sched_getaffinity(0))
+    quota = cgroup_cpus()
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)  # the harness's CPU share when no quota is readable
+    return min(nproc, quota or share or nproc), nproc, quota, share
+
+
+def prefill_cpu_baseline(model="llama-3.2-3b", n=4096, budget_s=12.0):
+    """Config 4's CPU baseline: the reference's `-m perplexity` loop (main.cpp:174-184:
+    one OUTPUT_LOGITS forward per position, then log(sample_prob(next)), sampler.cpp:11-25)
+    restated by the oracle (orc_forward + orc_sample_prob) on the same synthetic
+    Llama-3.2-3B fp16 weights, on this host's CPUs. Bounded sample: positions 0.. at the
+    start of the context, then the same number at the end (pos n - k .., over a cache
+    filled with seeded fp16 K/V rows: attention reads rows, not how they were made), each
+    half given half the budget; the n-position pass time is the trapezoid of the two
+    per-position costs (the per-position cost is linear in kv_len)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import numpy as np
+
+    import oracle_py as O
+    from yalm_amd import models as M
+
+    threads, nproc, quota, share = cpu_threads()
+    cfg = M.PRESETS[model].with_(weight_dtype=M.F16, max_seq_len=n)
+    host = O.synth_host_tensors_fast(cfg, seed=5)
+    om = O.OracleModel(cfg, host)
+    O.set_threads(threads)
+    rng = np.random.default_rng(0)
+    toks = rng.integers(0, cfg.vocab_size, size=n + 1)
+
+    def run(p0):
+        done, lp, t0 = 0, 0.0, time.perf_counter()
+        while True:
+            lg = om.forward(int(toks[p0 + done]), p0 + done, 1)
+            lp += float(np.log(O.olib.orc_sample_prob(O.P(lg), cfg.vocab_size, int(toks[p0 + done + 1]))))
+            done += 1
+            el = time.perf_counter() - t0
+            if (el >= budget_s / 2 and done >= 2) or done >= 64:
+                return done, el / done
+
+    k_head, s_head = run(0)
+    late = n - 64
+    for l in range(cfg.n_layers):  # the cache rows an n-position pass would hold before position `late`
+        om.kcache[l][:late] = (rng.standard_normal((late, cfg.kv_dim)) * 1.3).astype(np.float16)
+        om.vcache[l][:late] = (rng.standard_normal((late, cfg.kv_dim)) * 1.3).astype(np.float16)
+    k_tail, s_tail = run(late)
+    del om, host
+    total = (s_head + s_tail) / 2 * n
+    return {
+        "value": round(total * 1e3, 1),
+        "unit": "ms",
+        "cores": threads,
+        "kind": "port",
+        "ms_per_position": [round(s_head * 1e3, 2), round(s_tail * 1e3, 2)],
+        "cpu_model": cpu_model(),
+        "nproc": nproc,
+        "cgroup_cpus": quota,
+        "sample": f"oracle restatement of the reference -m perplexity loop (forward + sample_prob per position, "
+                  f"main.cpp:174-184), {model} fp16 synthetic weights: {k_head} positions from pos 0 and {k_tail} "
+                  f"from pos {late} ({threads} OpenMP threads); value = the {n}-position pass extrapolated "
+                  f"linearly in kv_len from the two per-position costs",
     }
 
 
@@ -614,6 +676,13 @@ def main():
             out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
         except Exception as e:  # report, never hide
             out["cpu_baseline"] = {"error": repr(e)}
+        if isinstance(out.get("prefill"), dict) and "error" not in out["prefill"]:
+            try:  # config 4's CPU baseline: the reference's sequential perplexity loop
+                pc = prefill_cpu_baseline(budget_s=args.cpu_seconds)
+                pc["speedup_gpu_vs_cpu"] = round(pc["value"] / out["prefill"]["value"], 1)
+                out["prefill"]["cpu_baseline"] = pc
+            except Exception as e:  # report, never hide
+                out["prefill"]["cpu_baseline"] = {"error": repr(e)[:300]}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

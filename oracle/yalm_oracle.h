@@ -7,16 +7,17 @@
  * cpu_baseline leg. Nothing in the product (yalm_amd/, include/yalm_hip.h)
  * links, loads or calls it; the product fails loudly without its HIP library.
  *
- * Pinning status: the reference's C++ CPU path cannot
- * be compiled in this image without stand-ins for absent headers
- * (cuda_runtime_api.h, spdlog); oracle/_ref builds only the reference
- * tokenizer (tokenizer.cpp needs neither). The
- * restatement is pinned by the reference's own known-answer test
- * (test.cpp:68-126, exact), by the reference's CPU-vs-GPU kernel test inputs
- * (test.cpp:148-206, regenerated bit-exactly with libstdc++), and by .yalm
- * fixtures produced by the reference's own convert.py. End-to-end forward
- * outputs are "parity partially pinned": cross-checked against an
- * independent float64 numpy forward in tests/.
+ * Pinning status: the reference's own CPU kernels are
+ * compiled here from /root/reference/src/infer.cpp unmodified (oracle/Makefile
+ * `ref-infer`: the genuine cuda_runtime_api.h that ships with triton satisfies
+ * model.h) and this restatement's orc_matmul_f32 / orc_matmul_f16 / orc_mha /
+ * orc_attn / orc_ffn are BIT-EXACT against their matmul_cpu / mha_cpu / ffn_cpu
+ * on the committed outputs (tests/test_ref_infer.py). The per-block glue
+ * (_block_cpu's rmsnorm, RoPE, clip, KV write, sink rotation, residual adds) and
+ * _forward_cpu need Block / Model objects from model.cpp, which needs spdlog
+ * (absent): restated statement by statement, cross-checked against an
+ * independent float64 numpy forward in tests/. Also pinned: the reference's
+ * known-answer test (test.cpp:68-126) and .yalm fixtures from its convert.py.
  *
  * Arithmetic follows the reference source statement by statement and is
  * compiled with the reference's flags (Makefile:36-39: -O3 -ffast-math -mavx2

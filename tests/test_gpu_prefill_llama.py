@@ -63,6 +63,35 @@ def test_prefill_llama3b_dims_vs_oracle():
     assert d_max <= LP_MAX, d_max
 
 
+@pytest.mark.parametrize("depth", [14, 28])
+def test_prefill_llama3b_full_depth_vs_oracle(depth):
+    """The real depth (28 layers; 14 as the midpoint of the depth curve) at the real
+    dims over 256 positions in one prefill pass, against the oracle's sequential
+    perplexity loop (main.cpp:174-184): the f16 activation rounding compounds with
+    depth, so the bars are checked where it is largest."""
+    cfg = M.LLAMA_32_3B.with_(n_layers=depth, max_seq_len=256)
+    n = 256
+    tokens = np.random.default_rng(1000 + depth).integers(0, cfg.vocab_size, size=n).astype(np.int32)
+    R = rt()
+    dm = R.DeviceModel.synthetic(cfg, seed=6)
+    dec = R.Decoder(dm)
+    try:
+        lp = dec.prefill(tokens)[: n - 1].astype(np.float64)
+    finally:
+        dec.close()
+        dm.close()
+    host = O.synth_host_tensors_fast(cfg, seed=6)
+    om = O.OracleModel(cfg, host)
+    lo = oracle_logprobs(om, tokens)
+    d = np.abs(lp - lo)
+    d_ppl = abs(lp.mean() - lo.mean())
+    print(f"llama-3b dims, {depth} layers, {n} positions: |d log ppl| {d_ppl:.2e}, max |d log p| {d.max():.2e}, "
+          f"p99 {np.quantile(d, 0.99):.2e}, median {np.median(d):.2e}, log ppl {-lo.mean():.4f}")
+    assert np.all(np.isfinite(lp))
+    assert d_ppl <= LOGPPL_TOL, d_ppl
+    assert d.max() <= LP_MAX, d.max()
+
+
 def test_prefill_llama3b_full_4096_property():
     """The whole config-4 workload: 28 layers x 4096 positions in one pass. The
     oracle would take hours here, so the check is against the sequential HIP

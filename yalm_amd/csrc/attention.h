@@ -31,9 +31,13 @@
 
 #include <float.h>
 
+#include <type_traits>
+
 #include "device_common.h"
 
 #define ATTN_THREADS 256
+#define ATTN_SPLITS 32     // key-chunk splits (workgroups) per kv head
+#define ATTN_MAX_SPLITS 64 // the merger gathers one partial per lane
 #define ATTN_WAVES (ATTN_THREADS / YALM_WAVE)
 
 // Keys per workgroup. Small on purpose: one CU streams only ~50-100 GB/s, so
@@ -74,19 +78,6 @@ __device__ __forceinline__ unsigned long long gran_ld(const unsigned long long *
 // Tag of one attention launch's chunk partials: unique per (forward, layer).
 __device__ __forceinline__ unsigned attn_part_tag(const StepState *step, int layer, int n_layers) {
 	return step->epoch * (unsigned)n_layers + (unsigned)layer;
-}
-
-// Head outputs of the fused launch: `reps` copies, `stride` granules apart (one per
-// XCD-group of consumers, attn_wo.h AWO_GR), so the 256 consumer workgroups' reads
-// spread over `reps` x the addresses.
-template <bool GRAN>
-__device__ __forceinline__ void attn_out_rep(float *out, size_t i, float v, unsigned tag, int reps, size_t stride) {
-	if constexpr (GRAN) {
-		for (int r = 0; r < reps; ++r)
-			attn_out<true>(out, i + (size_t)r * stride, v, tag);
-	} else {
-		out[i] = v;
-	}
 }
 
 // Sum over each aligned group of LPK lanes (one K row's pieces, LPK = head_dim / 8
@@ -169,34 +160,34 @@ __device__ __forceinline__ float attn_wave_red(float v) {
 }
 
 // One workgroup's share of the split-KV attention: kv head g, key chunks s0,
-// s0 + S, ... `hook()` runs right after the speculative K/V and q loads are
-// issued (attn_wo.h issues its weight stream there, behind them in vmcnt order).
-// Returns true on the workgroup that wrote the final head outputs of kv head g
-// (the single-chunk writer or the merger); the result is workgroup-uniform.
-// D = head_dim (16 .. 256, a power of two); GT >= G.
+// s0 + S, ... (S = splits per kv head). With one workgroup holding keys (kv_len <=
+// CHUNK, or S = 1) it writes the normalised head outputs itself and returns true;
+// otherwise it publishes ONE partial per head (unnormalised o[D], max M, sum L) as
+// granules tagged ptag into part [n_heads][nsplit][D + 2] at split s0, and the
+// MERGER workgroups (attn_merge_body, dispatched after every attention workgroup)
+// fold them. D = head_dim (16 .. 256, a power of two); GT >= G.
 // GRAN: outputs as {value, gtag} granules into `out` read as unsigned long long[].
-// part: [n_heads][nsplit][D + 2] granules tagged ptag (attn_part_tag); err: bit 2
-// set if the merger's bounded wait gave up (results wrong, reported).
 // ts / trace_on: attn_wo.h's timeline stamps (thread 0) and the trace-only waits.
 //
-// Layout: each wave runs its 16 keys of the chunk to the end WITHOUT a
-// workgroup barrier -- lane (row group, piece) holds 8 dims of NK K/V rows; the
-// scores are reduced across the row's pieces with DPP, the softmax statistics
-// are per wave (max / sum across row groups with DPP and lane swaps), P is never
-// stored, and the P.V sums are reduced across row groups in registers (transposed
-// sum4_rows). One barrier per chunk then combines the 4 waves' (m, l, o) with
-// the flash-decoding rescaling. Before commit 59434d2 the partial dots, the scores and
-// the P.V partials went through LDS behind 4 barriers (~6700 shader clocks from the
-// loads landing to the head outputs; tools/attn_wo_trace.py).
-template <int D, int GT, bool GRAN, class Hook>
-// (no __restrict__ here: with it the K/V and q loads may legally sink below the
-// hook's asm barrier once inlined; the standalone kernel keeps it on its arguments)
-__device__ __forceinline__ bool attn_decode_body(bool active, int g, int s0, int S, const float *q, const uint16_t *kc,
+// Layout: each wave runs its 16 keys of every chunk to the end WITHOUT a workgroup
+// barrier -- lane (row group, piece) holds 8 dims of NK K/V rows; the scores are
+// reduced across the row's pieces with DPP, the softmax statistics are per wave
+// (max / sum across row groups with DPP and lane swaps), P is never stored, and the
+// P.V sums stay in registers. Across the workgroup's chunks the wave keeps a running
+// (max, sum, P.V) with the flash-decoding rescaling, and the next chunk's K/V rows
+// are loaded before the current one is computed, so a workgroup with several chunks
+// pays one load latency, not one per chunk. One barrier at the end combines the 4
+// waves. Round 3 published one partial per 64-key chunk and the last attention
+// workgroup merged them in serial batches of 8 (kv 4096: 64 partials, 8 dependent
+// round trips, 20 us standalone).
+template <int D, int GT, bool GRAN>
+// (no __restrict__ here: the standalone kernel keeps it on its arguments)
+__device__ __forceinline__ bool attn_decode_body(int g, int s0, int S, const float *q, const uint16_t *kc,
                                                  const uint16_t *vc, const StepState *step, int n_heads,
                                                  int n_kv_heads, int max_seq_len, int nsplit, unsigned long long *part,
                                                  unsigned ptag, unsigned *err, float *out, float *att_dbg,
-                                                 Hook &&hook, unsigned gtag = 0, int greps = 1,
-                                                 unsigned long long *ts = nullptr, bool trace_on = false) {
+                                                 unsigned gtag = 0, unsigned long long *ts = nullptr,
+                                                 bool trace_on = false) {
 	constexpr int CHUNK = attn_chunk<D>();
 	constexpr int LPK = D / 8;                      // lanes per K/V row, 16 B each
 	static_assert(LPK >= 2 && LPK <= 32 && (LPK & (LPK - 1)) == 0, "head_dim 16 .. 256, a power of two");
@@ -217,10 +208,10 @@ __device__ __forceinline__ bool attn_decode_body(bool active, int g, int s0, int
 	const int piece = lane % LPK;
 	const int tl0 = wave * KPW + sub;
 
-	auto load_kv = [&](int t0, u32x4_t (&kw)[NK], u32x4_t (&vw)[NK]) {
+	auto load_kv = [&](int t0, int tmax, u32x4_t (&kw)[NK], u32x4_t (&vw)[NK]) {
 #pragma unroll
 		for (int i = 0; i < NK; ++i) {
-			const int t = min(t0 + tl0 + i * RSTEP, max_seq_len - 1);
+			const int t = min(t0 + tl0 + i * RSTEP, tmax);
 			const size_t off = (size_t)t * kv_dim + g * D + piece * 8;
 			kw[i] = load16(kc + off);
 			vw[i] = load16(vc + off);
@@ -233,10 +224,9 @@ __device__ __forceinline__ bool attn_decode_body(bool active, int g, int s0, int
 #pragma unroll
 	for (int j = 0; j < QL; ++j)
 		qv[j] = *(const float4_t *)(q + (size_t)g * gq + min((j * 64 + lane) * 4, gq - 4));
-	u32x4_t kw[NK], vw[NK];
-	load_kv(s0 * CHUNK, kw, vw);
-	const int kv_len = step->kv_len; // issued before the hook's loads: its wait must not cover them
-	hook();
+	u32x4_t kA[NK], vA[NK];
+	load_kv(s0 * CHUNK, max_seq_len - 1, kA, vA);
+	const int kv_len = step->kv_len;
 	// trace (attn_wo.h, thread 0 only): s_memrealtime + shader clock (s_memtime) at
 	// checkpoint k, kept in registers and stored at the end -- a store issued mid-way
 	// would queue behind the co-resident Wo workgroup's weight loads and stall the wave
@@ -255,7 +245,7 @@ __device__ __forceinline__ bool attn_decode_body(bool active, int g, int s0, int
 					ts[k] = tsr[k], ts[8 + k] = tsc[k];
 		}
 	};
-	if (!active || s0 * CHUNK >= kv_len) {
+	if (s0 * CHUNK >= kv_len) {
 		flush();
 		return false; // whole workgroup leaves before any barrier
 	}
@@ -280,19 +270,26 @@ __device__ __forceinline__ bool attn_decode_body(bool active, int g, int s0, int
 		qr[h][4] = b[0], qr[h][5] = b[1], qr[h][6] = b[2], qr[h][7] = b[3];
 	}
 	const int ns = (kv_len + CHUNK - 1) / CHUNK;
+	const int nact = min(ns, S); // workgroups of kv head g with keys: one partial each
 	const float sq = sqrtf((float)D);
 
-	// chunks s0, s0 + S, ... (S = gridDim.y splits; one pass for kv_len <= S * CHUNK)
-	for (int cidx = s0; cidx < ns; cidx += S) {
-		const int t0 = cidx * CHUNK;
-		if (cidx != s0)
-			load_kv(t0, kw, vw);
-		const int nt = min(CHUNK, kv_len - t0);
-		float acc[GT * 8]; // this lane's P.V sums: element e of head h at dim piece * 8 + e
+	// running state of this wave over its chunks: P.V sums (element e of head h at dim
+	// piece * 8 + e, not yet reduced across row groups), and per head the running max and
+	// sum of exponentials (head_dim 128: lane p of each 16-lane row holds head p % GT's;
+	// otherwise every lane holds all heads')
+	float acc[GT * 8];
 #pragma unroll
-		for (int k = 0; k < GT * 8; ++k)
-			acc[k] = 0.0f;
+	for (int k = 0; k < GT * 8; ++k)
+		acc[k] = 0.0f;
+	float Mr = -FLT_MAX, Lr = 0.0f, mw[GT], lw[GT];
+#pragma unroll
+	for (int h = 0; h < GT; ++h)
+		mw[h] = -FLT_MAX, lw[h] = 0.0f;
 
+	// FIRST: the workgroup's first chunk (nothing to rescale yet)
+	auto chunk = [&](auto first, const u32x4_t (&kw)[NK], const u32x4_t (&vw)[NK], int t0) {
+		constexpr bool FIRST = decltype(first)::value;
+		const int nt = min(CHUNK, kv_len - t0);
 		if constexpr (LPK == 16) {
 			// ---- head_dim 128: the row's 16 lanes share out its NK * GT scores (V values,
 			// padded to 16 J): a 4-step reduce-scatter of the partial dots leaves lane p of
@@ -330,24 +327,35 @@ __device__ __forceinline__ bool attn_decode_body(bool active, int g, int s0, int
 				ok[j] = f < V && tl0 + i * RSTEP < nt;
 				sc[j] = sc[j] / sq;
 				m = ok[j] ? fmaxf(m, sc[j]) : m;
-				if (att_dbg && ok[j] && h < G) // test hook: raw scores (normalised after the barrier)
+				if (att_dbg && ok[j] && h < G) // test hook: raw scores (normalised by the writer)
 					st_sc1(att_dbg + (size_t)(g * G + h) * max_seq_len + t0 + tl0 + i * RSTEP, sc[j]);
 			}
 			stamp(4);
-			// ---- per-wave softmax statistics of head h: over the row's lanes of the same
-			// head (row_ror by GT, 2 GT, ..), then over the 4 rows
+			// ---- per-wave softmax statistics of head h over the row's lanes of the same
+			// head (row_ror by GT, 2 GT, ..) and the 4 rows, folded into the running ones
 			m = attn_wave_red<GT, true>(m);
+			const float Mn = FIRST ? m : fmaxf(Mr, m);
 			float pj[J], l = 0.0f;
 #pragma unroll
 			for (int j = 0; j < J; ++j) {
-				pj[j] = ok[j] ? expf(sc[j] - m) : 0.0f;
+				pj[j] = ok[j] ? expf(sc[j] - Mn) : 0.0f;
 				l += pj[j];
 			}
 			l = attn_wave_red<GT, false>(l);
-			if (lane < GT && lane < G) {
-				wml[wave][lane][0] = m;
-				wml[wave][lane][1] = l;
+			if constexpr (FIRST) {
+				Lr = l;
+			} else {
+				const float corr = expf(Mr - Mn);
+				Lr = fmaf(Lr, corr, l);
+#pragma unroll
+				for (int hh = 0; hh < GT; ++hh) { // head hh's factor from lane hh of the row
+					const float c = row_bcast16(corr, hh);
+#pragma unroll
+					for (int e = 0; e < 8; ++e)
+						acc[hh * 8 + e] *= c;
+				}
 			}
+			Mr = Mn;
 			stamp(5);
 			// ---- P.V: probability f is broadcast from lane f % 16 of each row (row_newbcast)
 #pragma unroll
@@ -382,7 +390,7 @@ __device__ __forceinline__ bool attn_decode_body(bool active, int g, int s0, int
 					sv[i][h] = attn_row_sum<LPK>(d) / sq;
 				}
 			}
-			if (att_dbg && piece == 0) { // test hook: raw scores (normalised after the barrier)
+			if (att_dbg && piece == 0) { // test hook: raw scores (normalised by the writer)
 #pragma unroll
 				for (int i = 0; i < NK; ++i)
 #pragma unroll
@@ -391,7 +399,6 @@ __device__ __forceinline__ bool attn_decode_body(bool active, int g, int s0, int
 							st_sc1(att_dbg + (size_t)(g * G + h) * max_seq_len + t0 + tl0 + i * RSTEP, sv[i][h]);
 			}
 			stamp(4);
-			float mw[GT], lw[GT];
 #pragma unroll
 			for (int h = 0; h < GT; ++h) {
 				float m = -FLT_MAX;
@@ -399,23 +406,24 @@ __device__ __forceinline__ bool attn_decode_body(bool active, int g, int s0, int
 				for (int i = 0; i < NK; ++i)
 					m = valid[i] ? fmaxf(m, sv[i][h]) : m;
 				m = attn_wave_red<LPK, true>(m);
+				const float Mn = FIRST ? m : fmaxf(mw[h], m);
 				float l = 0.0f;
 #pragma unroll
 				for (int i = 0; i < NK; ++i) {
-					sv[i][h] = valid[i] ? expf(sv[i][h] - m) : 0.0f;
+					sv[i][h] = valid[i] ? expf(sv[i][h] - Mn) : 0.0f;
 					l += sv[i][h];
 				}
-				mw[h] = m;
-				lw[h] = attn_wave_red<LPK, false>(l);
-			}
-			if (lane < GT && lane < G) {
-				float m = mw[0], l = lw[0];
+				l = attn_wave_red<LPK, false>(l);
+				if constexpr (FIRST) {
+					lw[h] = l;
+				} else {
+					const float corr = expf(mw[h] - Mn);
+					lw[h] = fmaf(lw[h], corr, l);
 #pragma unroll
-				for (int h = 1; h < GT; ++h)
-					if (lane == h)
-						m = mw[h], l = lw[h];
-				wml[wave][lane][0] = m;
-				wml[wave][lane][1] = l;
+					for (int e = 0; e < 8; ++e)
+						acc[h * 8 + e] *= corr;
+				}
+				mw[h] = Mn;
 			}
 			stamp(5);
 #pragma unroll
@@ -429,193 +437,255 @@ __device__ __forceinline__ bool attn_decode_body(bool active, int g, int s0, int
 						acc[h * 8 + e] = fmaf(sv[i][h], vf[e], acc[h * 8 + e]);
 			}
 		}
+	};
 
-		// ---- this wave's P.V sums over its row groups, into LDS
-		if constexpr (LPK <= 16) {
-			// the row groups inside each DPP row first (LPK < 16), then across the 4 DPP
-			// rows transposed: for value group k, lane `piece` of DPP row r holds value
-			// 4k + r of that piece summed over the wave (element e of head h: dim piece * 8 + e)
+	// chunks s0, s0 + S, ...: one chunk per workgroup up to kv_len S * CHUNK (straight-line
+	// loads); beyond it the next chunk's rows are loaded before the current one is computed
+	// (the prefetch past the last chunk re-reads row kv_len - 1: unconditional loads keep
+	// hipcc's vmcnt counting exact, a conditional one would drain to 0 before every load)
+	using T_ = std::true_type;
+	using F_ = std::false_type;
+	if (s0 + S >= ns) {
+		chunk(T_{}, kA, vA, s0 * CHUNK);
+	} else {
+		u32x4_t kB[NK], vB[NK];
+		load_kv((s0 + S) * CHUNK, kv_len - 1, kB, vB);
+		chunk(T_{}, kA, vA, s0 * CHUNK);
+		for (int c = s0 + S;; c += 2 * S) { // kB / vB hold chunk c
+			load_kv((c + S) * CHUNK, kv_len - 1, kA, vA);
+			chunk(F_{}, kB, vB, c * CHUNK);
+			if (c + S >= ns)
+				break;
+			load_kv((c + 2 * S) * CHUNK, kv_len - 1, kB, vB);
+			chunk(F_{}, kA, vA, (c + S) * CHUNK);
+			if (c + 2 * S >= ns)
+				break;
+		}
+	}
+
+	// ---- this wave's running (max, sum) and P.V sums over its row groups, into LDS
+	if constexpr (LPK == 16) {
+		if (lane < GT && lane < G) {
+			wml[wave][lane][0] = Mr;
+			wml[wave][lane][1] = Lr;
+		}
+	} else if (lane < G) {
+		float m = mw[0], l = lw[0];
 #pragma unroll
-			for (int k = 0; k < GT * 8; ++k)
-				acc[k] = attn_fold_row<LPK, false>(acc[k]);
+		for (int h = 1; h < GT; ++h)
+			if (lane == h)
+				m = mw[h], l = lw[h];
+		wml[wave][lane][0] = m;
+		wml[wave][lane][1] = l;
+	}
+	if constexpr (LPK <= 16) {
+		// the row groups inside each DPP row first (LPK < 16), then across the 4 DPP
+		// rows transposed: for value group k, lane `piece` of DPP row r holds value
+		// 4k + r of that piece summed over the wave (element e of head h: dim piece * 8 + e)
 #pragma unroll
-			for (int k = 0; k < GT * 2; ++k) {
-				const float v4[4] = {acc[4 * k], acc[4 * k + 1], acc[4 * k + 2], acc[4 * k + 3]};
-				const float s = sum4_rows(v4);
-				const int idx = 4 * k + (lane >> 4), h = idx >> 3, e = idx & 7;
-				if (h < G && (lane & 15) < LPK)
-					wsum[wave][h][(lane & 15) * 8 + e] = s;
-			}
-		} else { // LPK 32: two row groups, the wave's halves
+		for (int k = 0; k < GT * 8; ++k)
+			acc[k] = attn_fold_row<LPK, false>(acc[k]);
 #pragma unroll
-			for (int k = 0; k < GT * 8; ++k)
-				acc[k] += xor32(acc[k]);
-			if (lane < 32) {
+		for (int k = 0; k < GT * 2; ++k) {
+			const float v4[4] = {acc[4 * k], acc[4 * k + 1], acc[4 * k + 2], acc[4 * k + 3]};
+			const float s = sum4_rows(v4);
+			const int idx = 4 * k + (lane >> 4), h = idx >> 3, e = idx & 7;
+			if (h < G && (lane & 15) < LPK)
+				wsum[wave][h][(lane & 15) * 8 + e] = s;
+		}
+	} else { // LPK 32: two row groups, the wave's halves
 #pragma unroll
-				for (int h = 0; h < GT; ++h)
+		for (int k = 0; k < GT * 8; ++k)
+			acc[k] += xor32(acc[k]);
+		if (lane < 32) {
 #pragma unroll
-					for (int e = 0; e < 8; ++e)
-						if (h < G)
-							wsum[wave][h][lane * 8 + e] = acc[h * 8 + e];
+			for (int h = 0; h < GT; ++h)
+#pragma unroll
+				for (int e = 0; e < 8; ++e)
+					if (h < G)
+						wsum[wave][h][lane * 8 + e] = acc[h * 8 + e];
+		}
+	}
+	if (att_dbg) // test hook: every wave's raw scores visible before the barrier / the partials
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	__syncthreads();
+	stamp(6);
+
+	// ---- combine the waves (fixed order): o = sum_w e^(m_w - M) o_w, L likewise
+	for (int i = tid; i < G * D; i += ATTN_THREADS) {
+		const int h = i / D, d = i % D;
+		float M = wml[0][h][0];
+#pragma unroll
+		for (int w = 1; w < ATTN_WAVES; ++w)
+			M = fmaxf(M, wml[w][h][0]);
+		float o = 0.0f, L = 0.0f;
+#pragma unroll
+		for (int w = 0; w < ATTN_WAVES; ++w) {
+			const float c = expf(wml[w][h][0] - M); // 0 for a wave without valid rows (m_w = -FLT_MAX)
+			o = fmaf(wsum[w][h][d], c, o);
+			L = fmaf(wml[w][h][1], c, L);
+		}
+		if (nact == 1) { // the only workgroup with keys: normalise and write the head outputs
+			attn_out<GRAN>(out, (size_t)(g * G + h) * D + d, o / L, gtag);
+		} else { // this workgroup's partial (o[D], M, L per head) as tagged granules
+			const size_t pp = ((size_t)(g * G + h) * nsplit + s0) * (D + 2);
+			attn_out<true>((float *)part, pp + d, o, ptag);
+			if (d == 0) {
+				attn_out<true>((float *)part, pp + D, M, ptag);
+				attn_out<true>((float *)part, pp + D + 1, L, ptag);
 			}
 		}
-		if (att_dbg) // test hook: every wave's raw scores visible before the barrier
-			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-		__syncthreads();
-		stamp(6);
-
-		// ---- combine the waves (fixed order): o = sum_w e^(m_w - M) o_w, L likewise
-		for (int i = tid; i < G * D; i += ATTN_THREADS) {
-			const int h = i / D, d = i % D;
+	}
+	if (nact == 1 && att_dbg) { // test hook: raw scores -> probabilities
+		const int nt = kv_len;
+		for (int i = tid; i < G * nt; i += ATTN_THREADS) {
+			const int h = i / nt, t = i % nt;
 			float M = wml[0][h][0];
 #pragma unroll
 			for (int w = 1; w < ATTN_WAVES; ++w)
 				M = fmaxf(M, wml[w][h][0]);
-			float o = 0.0f, L = 0.0f;
+			float L = 0.0f;
 #pragma unroll
-			for (int w = 0; w < ATTN_WAVES; ++w) {
-				const float c = expf(wml[w][h][0] - M); // 0 for a wave without valid rows (m_w = -FLT_MAX)
-				o = fmaf(wsum[w][h][d], c, o);
-				L = fmaf(wml[w][h][1], c, L);
-			}
-			if (ns == 1) { // single chunk: normalise and write the head outputs directly
-				attn_out_rep<GRAN>(out, (size_t)(g * G + h) * D + d, o / L, gtag, greps, (size_t)n_heads * D);
-			} else { // this chunk's partial (o[D], M, L per head) as tagged granules
-				const size_t pp = ((size_t)(g * G + h) * nsplit + cidx) * (D + 2);
-				attn_out<true>((float *)part, pp + d, o, ptag);
-				if (d == 0) {
-					attn_out<true>((float *)part, pp + D, M, ptag);
-					attn_out<true>((float *)part, pp + D + 1, L, ptag);
-				}
-			}
-		}
-		if (ns == 1) {
-			if (att_dbg) { // test hook: raw scores -> probabilities
-				for (int i = tid; i < G * nt; i += ATTN_THREADS) {
-					const int h = i / nt, t = i % nt;
-					float M = wml[0][h][0];
-#pragma unroll
-					for (int w = 1; w < ATTN_WAVES; ++w)
-						M = fmaxf(M, wml[w][h][0]);
-					float L = 0.0f;
-#pragma unroll
-					for (int w = 0; w < ATTN_WAVES; ++w)
-						L = fmaf(wml[w][h][1], expf(wml[w][h][0] - M), L);
-					float *a = att_dbg + (size_t)(g * G + h) * max_seq_len + t;
-					*a = expf(ld_sc1(a) - M) / L;
-				}
-			}
-			flush();
-			return true;
-		}
-		if (cidx + S < ns)
-			__syncthreads(); // wsum / wml are rewritten by the next chunk
-	}
-	if (s0 != min(ns, S) - 1) {
-		flush();
-		return false; // not the merger: nothing to wait for
-	}
-
-	// ---- merger: gather the ns chunk partials of heads g*G .. as granules, re-reading
-	// a batch of MB chunks until every tag holds ptag (one round trip when the other
-	// workgroups are done, which they usually are: they started together), then merge
-	// in chunk order with the online rescaling of flash-decoding.
-	constexpr int MB = 8;
-	constexpr int DPL = D >= 64 ? D / 64 : 1; // dims per lane
-	const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + ATTN_TIMEOUT;
-	bool alive = true;
-	for (int h = wave; h < G; h += ATTN_WAVES) {
-		const unsigned long long *ph = part + (size_t)(g * G + h) * nsplit * (D + 2);
-		float M = -FLT_MAX, L = 0.0f, o[DPL];
-#pragma unroll
-		for (int k = 0; k < DPL; ++k)
-			o[k] = 0.0f;
-		const int dl = lane < D ? lane : 0; // lanes past D (D < 64) re-read dim 0 and only follow along
-		for (int c0 = 0; c0 < ns; c0 += MB) {
-			float mb[MB], lb[MB], ob[MB][DPL];
-			for (;;) {
-				unsigned long long gm[MB], gl[MB], go[MB][DPL];
-#pragma unroll
-				for (int j = 0; j < MB; ++j) {
-					const int c = min(c0 + j, ns - 1);
-					const unsigned long long *pc = ph + (size_t)c * (D + 2);
-					gm[j] = gran_ld(pc + D);
-					gl[j] = gran_ld(pc + D + 1);
-#pragma unroll
-					for (int k = 0; k < DPL; ++k)
-						go[j][k] = gran_ld(pc + dl + 64 * k);
-				}
-				bool ok = true;
-#pragma unroll
-				for (int j = 0; j < MB; ++j) {
-					ok = ok && (unsigned)(gm[j] >> 32) == ptag && (unsigned)(gl[j] >> 32) == ptag;
-#pragma unroll
-					for (int k = 0; k < DPL; ++k)
-						ok = ok && (unsigned)(go[j][k] >> 32) == ptag;
-					mb[j] = __uint_as_float((unsigned)gm[j]);
-					lb[j] = __uint_as_float((unsigned)gl[j]);
-#pragma unroll
-					for (int k = 0; k < DPL; ++k)
-						ob[j][k] = __uint_as_float((unsigned)go[j][k]);
-				}
-				if (__all(ok) || !alive)
-					break;
-				__builtin_amdgcn_s_sleep(1);
-				if (__builtin_amdgcn_s_memrealtime() > deadline) {
-					alive = false; // one more pass, then give up (results wrong, reported)
-					if (err && lane == 0)
-						__hip_atomic_fetch_or(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-				}
-			}
-			float Mn = M;
-#pragma unroll
-			for (int j = 0; j < MB; ++j)
-				if (c0 + j < ns)
-					Mn = fmaxf(Mn, mb[j]);
-			const float r = expf(M - Mn); // 0 on the first batch (M = -FLT_MAX)
-			L *= r;
-#pragma unroll
-			for (int k = 0; k < DPL; ++k)
-				o[k] *= r;
-#pragma unroll
-			for (int j = 0; j < MB; ++j) {
-				if (c0 + j < ns) {
-					const float w = expf(mb[j] - Mn);
-					L += w * lb[j];
-#pragma unroll
-					for (int k = 0; k < DPL; ++k)
-						o[k] += w * ob[j][k];
-				}
-			}
-			M = Mn;
-		}
-		stamp(7);
-		if (lane < D) {
-#pragma unroll
-			for (int k = 0; k < DPL; ++k)
-				attn_out_rep<GRAN>(out, (size_t)(g * G + h) * D + lane + 64 * k, o[k] / L, gtag, greps,
-				                   (size_t)n_heads * D);
-		}
-		if (att_dbg) {
-			for (int t = lane; t < kv_len; t += 64) {
-				float *a = att_dbg + (size_t)(g * G + h) * max_seq_len + t;
-				*a = expf(ld_sc1(a) - M) / L;
-			}
+			for (int w = 0; w < ATTN_WAVES; ++w)
+				L = fmaf(wml[w][h][1], expf(wml[w][h][0] - M), L);
+			float *a = att_dbg + (size_t)(g * G + h) * max_seq_len + t;
+			*a = expf(ld_sc1(a) - M) / L;
 		}
 	}
 	flush();
+	return nact == 1;
+}
+
+// MERGER workgroup of (kv head g, query head h = g * G + hq): with nact > 1
+// attention workgroups holding keys, gathers their nact partials of head h and
+// writes the normalised head output. Mergers are dispatched after every attention
+// workgroup of the launch, so they only wait on earlier ones (no deadlock however
+// few workgroups are resident). Wave w takes splits w, w + 4, ...: all its granule
+// loads (per lane 2 dims of each of its splits, and lane j the (M, L) of its j-th
+// split) are issued at once and re-read until every tag holds ptag; the waves'
+// (max, sum, o) meet in LDS and are folded in wave order (deterministic). One head
+// per workgroup: a merger gathers (D + 2) x 8 B per split (33 KB at kv 4096), where
+// the round-4 first cut merged all G heads of a kv head in ONE workgroup (131 KB
+// through one CU). Returns true if it wrote the head (nact > 1).
+template <int D, bool GRAN>
+__device__ __forceinline__ bool attn_merge_body(int g, int hq, int S, const StepState *step, int n_heads,
+                                                int n_kv_heads, int max_seq_len, int nsplit,
+                                                const unsigned long long *part, unsigned ptag, unsigned *err,
+                                                float *out, float *att_dbg, unsigned gtag = 0) {
+	constexpr int CHUNK = attn_chunk<D>();
+	constexpr int SPW = ATTN_MAX_SPLITS / ATTN_WAVES; // splits per wave, at most
+	constexpr int E = D >= 64 ? D / 64 : 1;           // dims per lane: lane + 64 k
+	__shared__ float mml[ATTN_WAVES][2];
+	__shared__ float mo[ATTN_WAVES][D];
+	const int G = n_heads / n_kv_heads;
+	const int h = g * G + hq;
+	const int kv_len = step->kv_len;
+	const int ns = (kv_len + CHUNK - 1) / CHUNK;
+	const int nact = min(ns, S);
+	if (nact <= 1 || hq >= G)
+		return false;
+	const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+	const int nsw = (nact - wave + ATTN_WAVES - 1) / ATTN_WAVES; // this wave's splits: wave + 4 j, j < nsw
+	const int dl = lane < D ? lane : 0; // lanes past D (D < 64) re-read dim 0 and only follow along
+	const unsigned long long *ph = part + (size_t)h * nsplit * (D + 2);
+	const unsigned long long *pl = ph + (size_t)(wave + ATTN_WAVES * min(lane, max(nsw - 1, 0))) * (D + 2);
+	const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + ATTN_TIMEOUT;
+	bool alive = true;
+	float ms = -FLT_MAX, ls = 0.0f, ob[SPW][E];
+	for (;;) {
+		unsigned long long gm = 0, gl = 0, go[SPW][E];
+		if (nsw > 0) {
+			gm = gran_ld(pl + D);
+			gl = gran_ld(pl + D + 1);
+		}
+#pragma unroll
+		for (int j = 0; j < SPW; ++j) {
+			if (j < nsw) {
+				const unsigned long long *pc = ph + (size_t)(wave + ATTN_WAVES * j) * (D + 2);
+#pragma unroll
+				for (int k = 0; k < E; ++k)
+					go[j][k] = gran_ld(pc + dl + 64 * k);
+			}
+		}
+		bool ok = lane >= nsw || ((unsigned)(gm >> 32) == ptag && (unsigned)(gl >> 32) == ptag);
+#pragma unroll
+		for (int j = 0; j < SPW; ++j) {
+			if (j < nsw) {
+#pragma unroll
+				for (int k = 0; k < E; ++k) {
+					ok = ok && (unsigned)(go[j][k] >> 32) == ptag;
+					ob[j][k] = __uint_as_float((unsigned)go[j][k]);
+				}
+			}
+		}
+		if (lane < nsw) {
+			ms = __uint_as_float((unsigned)gm);
+			ls = __uint_as_float((unsigned)gl);
+		}
+		if (__all(ok) || !alive)
+			break;
+		__builtin_amdgcn_s_sleep(1);
+		if (__builtin_amdgcn_s_memrealtime() > deadline) {
+			alive = false; // one more pass, then give up (results wrong, reported)
+			if (err && lane == 0)
+				__hip_atomic_fetch_or(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		}
+	}
+	// this wave's max, then the workgroup's (LDS), the weights e^(m_s - M) on lane j
+	const float mw = wave_max(ms);
+	if (lane == 0)
+		mml[wave][0] = mw;
+	__syncthreads();
+	const float M = fmaxf(fmaxf(mml[0][0], mml[1][0]), fmaxf(mml[2][0], mml[3][0]));
+	const float ws = lane < nsw ? expf(ms - M) : 0.0f;
+	const float lw = wave_sum(ws * ls);
+	float o[E];
+#pragma unroll
+	for (int k = 0; k < E; ++k)
+		o[k] = 0.0f;
+#pragma unroll
+	for (int j = 0; j < SPW; ++j) {
+		if (j < nsw) {
+			const float w = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ws), j));
+#pragma unroll
+			for (int k = 0; k < E; ++k)
+				o[k] = fmaf(w, ob[j][k], o[k]);
+		}
+	}
+	if (lane < D) {
+#pragma unroll
+		for (int k = 0; k < E; ++k)
+			mo[wave][lane + 64 * k] = o[k];
+	}
+	if (lane == 0)
+		mml[wave][1] = lw;
+	__syncthreads();
+	const float L = (mml[0][1] + mml[1][1]) + (mml[2][1] + mml[3][1]);
+	for (int d = tid; d < D; d += ATTN_THREADS)
+		attn_out<GRAN>(out, (size_t)h * D + d, ((mo[0][d] + mo[1][d]) + (mo[2][d] + mo[3][d])) / L, gtag);
+	if (att_dbg) {
+		for (int t = tid; t < kv_len; t += ATTN_THREADS) {
+			float *a = att_dbg + (size_t)h * max_seq_len + t;
+			*a = expf(ld_sc1(a) - M) / L;
+		}
+	}
 	return true;
 }
 
-// grid (n_kv_heads, S): workgroup (g, s) is dispatched after (g', s') for every
-// s' < s, so the merger (the highest s with work) only waits on earlier ones.
+// Grid: n_kv * S attention workgroups (b = g + n_kv * s: (g, s) is dispatched after
+// (g', s') for every s' < s), then n_kv * G merger workgroups (g, hq).
 template <int D, int GT>
 __global__ __launch_bounds__(ATTN_THREADS) void attn_decode_kernel(
     const float *__restrict__ q, const uint16_t *__restrict__ kc, const uint16_t *__restrict__ vc,
-    const StepState *__restrict__ step, int n_heads, int n_kv_heads, int max_seq_len, int nsplit,
+    const StepState *__restrict__ step, int n_heads, int n_kv_heads, int max_seq_len, int nsplit, int S,
     unsigned long long *__restrict__ part, int layer, int n_layers, unsigned *__restrict__ err,
     float *__restrict__ out, float *__restrict__ att_dbg) {
-	attn_decode_body<D, GT, false>(true, blockIdx.x, blockIdx.y, gridDim.y, q, kc, vc, step, n_heads, n_kv_heads,
-	                               max_seq_len, nsplit, part, attn_part_tag(step, layer, n_layers), err, out, att_dbg,
-	                               [] {});
+	const int b = blockIdx.x, units = n_kv_heads * S;
+	const unsigned ptag = attn_part_tag(step, layer, n_layers);
+	if (b < units)
+		attn_decode_body<D, GT, false>(b % n_kv_heads, b / n_kv_heads, S, q, kc, vc, step, n_heads, n_kv_heads,
+		                               max_seq_len, nsplit, part, ptag, err, out, att_dbg);
+	else
+		attn_merge_body<D, false>((b - units) % n_kv_heads, (b - units) / n_kv_heads, S, step, n_heads, n_kv_heads,
+		                          max_seq_len, nsplit, part, ptag, err, out, att_dbg);
 }

@@ -5,15 +5,16 @@
 // carries only the (small) KV read, and the Wo GEMV that follows starts its
 // 33.5 MB stream (Mistral-7B fp16) from a cold pipe. Here one grid holds two
 // kinds of workgroups:
-//   * ATTENTION workgroups [0, n_kv * S): attn_decode_body (attention.h); the
-//     workgroup that finishes kv head g (single-chunk writer or last arriver of
-//     the split-KV merge) writes each head-output element as an 8-byte
+//   * ATTENTION workgroups [0, n_kv * S): attn_decode_body (attention.h), then
+//     n_kv * G MERGER workgroups (attn_merge_body); the workgroup that finishes
+//     a head (the single attention workgroup holding keys, or the head's merger)
+//     writes each head-output element as an 8-byte
 //     {value, epoch} GRANULE with ONE sc1 store into this layer's granule buffer:
 //     the data is its own ready flag (MI355X_MICROARCH.md §visibility, R2
 //     granule), so there is no drain (vmcnt(0)) and no separate flag store.
 //     They issue no weight loads: a weight stream queued in front of the merge's
 //     loads (vmcnt is in order) would hold the whole hand-off behind it.
-//   * Wo workgroups [n_kv * S, grid): each owns AWO_RPW contiguous Wo rows and
+//   * Wo workgroups [n_kv * (S + G), grid): each owns AWO_RPW contiguous Wo rows and
 //     issues them as register loads at once, so the 33.5 MB stream runs while
 //     the attention works. Each WAVE then gathers its input columns' granules
 //     with 16-byte sc1 loads (two granules each), re-reading a batch until every
@@ -42,7 +43,6 @@
 #define AWO_RPW 16                   // Wo rows per Wo workgroup (256 of them for Mistral-7B)
 #define AWO_TIMEOUT 200000000ull     // 2 s of s_memrealtime (100 MHz)
 #define AWO_REPL_STRIDE 32           // words of the error slot (a 128-B line of its own)
-#define AWO_GR 8                     // max copies of the head outputs per layer (one per XCD)
 #define AWO_TRACE_N 16               // s_memrealtime + s_memtime stamps per workgroup (yalm_attn_wo_trace)
 
 struct AttnWoArgs {
@@ -55,12 +55,8 @@ struct AttnWoArgs {
 	float *x;           // residual stream (dim)
 	unsigned *err;      // error bits (bounded spin gave up)
 	unsigned long long *trace; // [grid][AWO_TRACE_N] s_memrealtime stamps (YALM_ATTN_WO_TRACE=1) or null
-	int win;            // Wo loads in flight per lane: 0 = all at once, 8 / 16 / 24 (YALM_ATTN_WO_WIN);
-	                    // -1 = no weight loads (YALM_ABLATE bit 32, timing only: results wrong)
 	int delay;          // s_memrealtime ticks (10 ns) the Wo workgroups wait before their slice loads
-	                    // (YALM_ATTN_WO_DELAY, tuning knob: lets the attention chain start alone)
-	int spec;           // speculative gather once the slice has landed (YALM_AWO_SPEC)
-	int greps;          // copies of the head outputs (YALM_AWO_REPL, <= AWO_GR); Wo workgroup j reads copy j % greps
+	                    // (lets the attention's K/V and q loads reach HBM first)
 };
 
 // Eight 16-byte sc1 loads from arbitrary addresses in one statement, one vmcnt(0)
@@ -88,25 +84,6 @@ __device__ __forceinline__ void awo_ld8_sc1(u32x4_t (&v)[8], const void *const (
 	             : "memory");
 }
 
-// The same eight loads plus one 8-byte sc1 load of a sentinel granule, one vmcnt(0).
-__device__ __forceinline__ void awo_ld8s_sc1(u32x4_t (&v)[8], const void *const (&a)[8], unsigned long long &sv,
-                                             const void *sp) {
-	asm volatile("global_load_dwordx4 %0, %9, off sc1\n\t"
-	             "global_load_dwordx4 %1, %10, off sc1\n\t"
-	             "global_load_dwordx4 %2, %11, off sc1\n\t"
-	             "global_load_dwordx4 %3, %12, off sc1\n\t"
-	             "global_load_dwordx4 %4, %13, off sc1\n\t"
-	             "global_load_dwordx4 %5, %14, off sc1\n\t"
-	             "global_load_dwordx4 %6, %15, off sc1\n\t"
-	             "global_load_dwordx4 %7, %16, off sc1\n\t"
-	             "global_load_dwordx2 %8, %17, off sc1\n\t"
-	             "s_waitcnt vmcnt(0)"
-	             : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]),
-	               "=&v"(v[7]), "=&v"(sv)
-	             : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "v"(sp)
-	             : "memory");
-}
-
 // This lane's XS pieces of the attention output (EPL columns each, pieces
 // ATTN_THREADS * EPL columns apart) as {value, tag} granules, gathered with
 // 16-byte sc1 loads (two granules each) in batches of 8, each batch re-read until
@@ -115,16 +92,15 @@ __device__ __forceinline__ void awo_ld8s_sc1(u32x4_t (&v)[8], const void *const 
 // when the memory system executes it, so one issued at launch start (behind the
 // slice in the CU's queue, its result usable only once the slice is in, vmcnt
 // being in order) would return a stale sample and cost a second round trip.
-// First attempt: batch 0 together with one sentinel granule per covered head (the
-// head's last element). All tags fresh: done in ONE round trip (the heads are
-// usually written by the time the slice lands). Otherwise, if the sentinels are
-// fresh, only the re-gather is left; if not, the cheap sentinel poll (one 8-byte
-// load per lane) runs before the full re-reads. `spec` = 0 (YALM_AWO_SPEC=0)
-// skips the combined first attempt. False if the bounded spin gave up (deadline,
+// First the cheap sentinel poll (one 8-byte load per lane: the last element of
+// each covered head), then the gather. Round 3 measured a combined first attempt
+// (gather + sentinels in one round trip) slower: 1024 waves gathering the same
+// 32 KB of granules as the slices land is a burst the poll avoids
+// (profiles/r3_ab_awo.txt). False if the bounded spin gave up (deadline,
 // s_memrealtime).
 template <int EPL, int XS>
 __device__ __forceinline__ bool awo_gather_gran(float (&xs)[XS][EPL], const unsigned long long *gran, int tid,
-                                                unsigned tag, unsigned long long deadline, bool spec) {
+                                                unsigned tag, unsigned long long deadline) {
 	constexpr int LPP = EPL / 2;   // 16-byte loads per piece
 	constexpr int NL = XS * LPP;   // 4, 8 or 16
 	constexpr int NB = (NL + 7) / 8;
@@ -139,15 +115,39 @@ __device__ __forceinline__ bool awo_gather_gran(float (&xs)[XS][EPL], const unsi
 		const int h = (k * ATTN_THREADS + 64 * wave) * EPL / D + l % HPP;
 		sent = gran + (size_t)h * D + (D - 1);
 	}
-	auto addrs = [&](int bt, const void *(&a)[8]) {
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the slice has landed
+	for (;;) {
+		const unsigned long long g = __hip_atomic_load(sent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		if (__all((unsigned)(g >> 32) == tag))
+			break;
+		__builtin_amdgcn_s_sleep(1);
+		if (__builtin_amdgcn_s_memrealtime() > deadline) {
+			alive = false;
+			break;
+		}
+	}
+#pragma unroll
+	for (int bt = 0; bt < NB; ++bt) {
+		const void *a[8];
 #pragma unroll
 		for (int i = 0; i < 8; ++i) {
 			const int l = bt * 8 + (i < NL - bt * 8 ? i : 0); // pad a short batch with a repeat
 			const int k = l / LPP, e = (l % LPP) * 2;
 			a[i] = gran + (size_t)(k * ATTN_THREADS + tid) * EPL + e;
 		}
-	};
-	auto take = [&](int bt, const u32x4_t (&v)[8]) {
+		u32x4_t v[8];
+		for (;;) {
+			awo_ld8_sc1(v, a);
+			bool ok = true;
+#pragma unroll
+			for (int i = 0; i < 8; ++i)
+				ok = ok && v[i][1] == tag && v[i][3] == tag;
+			if (__all(ok) || !alive)
+				break;
+			__builtin_amdgcn_s_sleep(1);
+			if (__builtin_amdgcn_s_memrealtime() > deadline)
+				alive = false; // one more pass, then give up (results wrong, reported)
+		}
 #pragma unroll
 		for (int i = 0; i < 8; ++i) {
 			if (i < NL - bt * 8) {
@@ -158,59 +158,6 @@ __device__ __forceinline__ bool awo_gather_gran(float (&xs)[XS][EPL], const unsi
 				xs[k][e + 1] = __uint_as_float(w1);
 			}
 		}
-	};
-	auto fresh = [&](const u32x4_t (&v)[8]) {
-		bool ok = true;
-#pragma unroll
-		for (int i = 0; i < 8; ++i)
-			ok = ok && v[i][1] == tag && v[i][3] == tag;
-		return __all(ok);
-	};
-	asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the slice has landed
-	bool sent_ok = false;
-	int bt0 = 0;
-	if (spec) {
-		const void *a[8];
-		addrs(0, a);
-		u32x4_t v[8];
-		unsigned long long sv;
-		awo_ld8s_sc1(v, a, sv, sent);
-		sent_ok = __all((unsigned)(sv >> 32) == tag);
-		if (fresh(v)) {
-			take(0, v);
-			bt0 = 1;
-			if (NB == 1)
-				return true;
-		}
-	}
-	if (!sent_ok) {
-		for (;;) {
-			const unsigned long long g = __hip_atomic_load(sent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-			if (__all((unsigned)(g >> 32) == tag))
-				break;
-			__builtin_amdgcn_s_sleep(1);
-			if (__builtin_amdgcn_s_memrealtime() > deadline) {
-				alive = false;
-				break;
-			}
-		}
-	}
-#pragma unroll
-	for (int bt = 0; bt < NB; ++bt) {
-		if (bt < bt0)
-			continue;
-		const void *a[8];
-		addrs(bt, a);
-		u32x4_t v[8];
-		for (;;) {
-			awo_ld8_sc1(v, a);
-			if (fresh(v) || !alive)
-				break;
-			__builtin_amdgcn_s_sleep(1);
-			if (__builtin_amdgcn_s_memrealtime() > deadline)
-				alive = false; // one more pass, then give up (results wrong, reported)
-		}
-		take(bt, v);
 	}
 	return alive;
 }
@@ -225,7 +172,8 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 	constexpr int LPT = AWO_RPW * XS;
 	static_assert(ATTN_THREADS == 256 && ATTN_WAVES == 4, "4-wave workgroups: one 4-row reduction per wave");
 	const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-	const int units = p.n_kv * p.S;
+	const int units = p.n_kv * p.S;                      // attention workgroups
+	const int munits = units + p.n_kv * (p.n_heads / p.n_kv); // + one merger per query head
 	// include/yalm_hip.h yalm_attn_wo_trace: [0] start, [1] hand-off signalled / Wo slice landed, ...
 	// (kept in registers, stored when the workgroup is done: see attention.h `stamp`)
 	unsigned long long *tr = p.trace && tid == 0 ? p.trace + (size_t)b * AWO_TRACE_N : nullptr;
@@ -234,10 +182,15 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 		t_start = __builtin_amdgcn_s_memrealtime(), c_start = __builtin_amdgcn_s_memtime();
 
 	const unsigned epoch = step->epoch; // this launch's tag (step_begin_kernel / set_step_full_kernel)
-	if (b < units) { // ---- attention workgroup
-		const bool wrote = attn_decode_body<D, GT, true>(
-		    true, b % p.n_kv, b / p.n_kv, p.S, q, kc, vc, step, p.n_heads, p.n_kv, p.max_seq_len, p.nsplit, p.part,
-		    epoch * (unsigned)p.n_layers + (unsigned)p.layer, p.err, (float *)p.gran, nullptr, [] {}, epoch, p.greps, tr, p.trace != nullptr);
+	if (b < munits) { // ---- attention or merger workgroup
+		const unsigned ptag = epoch * (unsigned)p.n_layers + (unsigned)p.layer;
+		const bool wrote =
+		    b < units ? attn_decode_body<D, GT, true>(b % p.n_kv, b / p.n_kv, p.S, q, kc, vc, step, p.n_heads, p.n_kv,
+		                                               p.max_seq_len, p.nsplit, p.part, ptag, p.err, (float *)p.gran,
+		                                               nullptr, epoch, tr, p.trace != nullptr)
+		              : attn_merge_body<D, true>((b - units) % p.n_kv, (b - units) / p.n_kv, p.S, step, p.n_heads,
+		                                         p.n_kv, p.max_seq_len, p.nsplit, p.part, ptag, p.err,
+		                                         (float *)p.gran, nullptr, epoch);
 		if (tr) { // the head outputs are their own ready flags: nothing to drain or signal
 			const unsigned long long t1 = __builtin_amdgcn_s_memrealtime(), c1 = __builtin_amdgcn_s_memtime();
 			tr[0] = t_start, tr[8] = c_start;
@@ -249,7 +202,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 
 	// ---- Wo workgroup j
 	__shared__ float rowpart[AWO_RPW][ATTN_WAVES];
-	const int j = b - units;
+	const int j = b - munits;
 	const int row0 = j * AWO_RPW;
 	// the last slice may run past the matrix: shifted back so every load stays in
 	// bounds (unconditional loads); rows below row0 belong to workgroup j - 1
@@ -261,20 +214,9 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 			__builtin_amdgcn_s_sleep(2);
 	}
 	u32x4_t wr[LPT];
-	// p.win > 0: at most win loads in flight per lane (a sliding window), so the
-	// slice does not fill the CU's memory queues ahead of the attention's loads
 #pragma unroll
-	for (int i = 0; i < LPT; ++i) {
-		if (i >= 8) {
-			if (p.win == 8)
-				asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-			else if (p.win == 16 && i >= 16)
-				asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
-			else if (p.win == 24 && i >= 24)
-				asm volatile("s_waitcnt vmcnt(23)" ::: "memory");
-		}
-		wr[i] = p.win >= 0 ? load_nt16(wbase + ((size_t)i * ATTN_THREADS + tid) * 16) : u32x4_t{0u, 0u, 0u, 0u};
-	}
+	for (int i = 0; i < LPT; ++i)
+		wr[i] = load_nt16(wbase + ((size_t)i * ATTN_THREADS + tid) * 16);
 	unsigned long long t_slice = 0, c_slice = 0, t_poll = 0, c_poll = 0;
 	if (tr) { // tracing only: when the whole slice has landed
 		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -286,8 +228,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 	// only for the heads its columns cover), then dot them into every resident row.
 	const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 	float xs[XS][EPL];
-	const unsigned long long *gran = p.gran + (size_t)(j % p.greps) * p.q_dim;
-	if (!awo_gather_gran<EPL, XS>(xs, gran, tid, epoch, t0 + AWO_TIMEOUT, p.spec != 0) && lane == 0)
+	if (!awo_gather_gran<EPL, XS>(xs, p.gran, tid, epoch, t0 + AWO_TIMEOUT) && lane == 0)
 		__hip_atomic_fetch_or(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 	if (tr)
 		t_poll = __builtin_amdgcn_s_memrealtime(), c_poll = __builtin_amdgcn_s_memtime();

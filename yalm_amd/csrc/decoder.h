@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -46,6 +47,20 @@ enum { GK_QKV = 0, GK_WO = 1, GK_GLU = 2, GK_W2 = 3, GK_CLS = 4, GK_N = 5 };
 
 int device_cu_count();
 
+// Tuning / tracing knobs are read from the environment only in the A/B build
+// (tools/build_ab_lib.sh compiles with -DYALM_AB): the production library's
+// behaviour depends on none of them. Functional switches (YALM_ATTN_WO=0: separate
+// attention and Wo launches; YALM_EAGER / YALM_GRAPH_SYNC: launch mode) are read once
+// at decoder creation in every build.
+inline const char *ab_env(const char *name) {
+#ifdef YALM_AB
+	return getenv(name);
+#else
+	(void)name;
+	return nullptr;
+#endif
+}
+
 // Batched-prefill scratch (prefill.hip), allocated on first use for
 // max_seq_len rows.
 struct PrefillBufs {
@@ -86,8 +101,6 @@ struct yalm_decoder_s {
 	GemvCfg gemv[GK_N];
 	bool eager = false;     // YALM_EAGER=1: launch kernels directly (profilers that mis-handle graph replay)
 	bool graph_sync = false; // YALM_GRAPH_SYNC=1: synchronise after every replay
-	int ablate = 0;          // YALM_ABLATE bitmask: skip qkv|attn|wo|glu|w2 (1|2|4|8|16), or (32) load no Wo
-	                         // weights in the fused attention + Wo launch; timing only, results wrong
 	std::string kname;
 	PrefillBufs pf;
 	// tensor parallelism (yalm_decoder_create_tp): c holds the LOCAL shard dims
@@ -111,12 +124,9 @@ struct yalm_decoder_s {
 	bool attn_wo = false;
 	int awo_nb = 0;                  // grid: n_kv * awo_S attention + ceil(dim / AWO_RPW) Wo workgroups
 	int awo_S = 0;                   // key-chunk splits per kv head
-	unsigned long long *awo_trace = nullptr; // YALM_ATTN_WO_TRACE=1: [grid][4] stamps of the last launch
-	int awo_win = 0;                 // Wo loads in flight per lane (YALM_ATTN_WO_WIN), -1 = none (ablation)
-	int awo_delay = 0;               // ticks the Wo workgroups wait before their slice loads (YALM_ATTN_WO_DELAY)
-	int awo_spec = 0;                // YALM_AWO_SPEC=1: speculative gather after the slice landed (attn_wo.h)
-	unsigned long long *awo_gran = nullptr; // [n_layers][AWO_GR][q_dim] attention outputs as {value, epoch} granules
-	int awo_greps = 1;               // copies written / read (YALM_AWO_REPL)
+	unsigned long long *awo_trace = nullptr; // A/B build, YALM_ATTN_WO_TRACE=1: [grid][16] stamps of the last launch
+	int awo_delay = 0;               // ticks the Wo workgroups wait before their slice loads
+	unsigned long long *awo_gran = nullptr; // [n_layers][q_dim] attention outputs as {value, epoch} granules
 	unsigned *awo_err = nullptr;     // error word of the in-launch waits (bit 0 fused Wo gather, bit 1 attention merger)
 };
 

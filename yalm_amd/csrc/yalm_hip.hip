@@ -156,7 +156,7 @@ static int launch_rb_t(const P &p, const float *x, const float *normw, float eps
 		// per wave (profiles/r3_gemv_rows.txt: W1|W3 fp16 39.4-40.0 -> 36.9 us, fp8 W2 13.4 ->
 		// 12.7-13.0; fp16 W2 with ONE 28-KB row per wave went 20.3 -> 21.3, so it keeps the
 		// chunk order); YALM_GEMV_ROWS=0 keeps the chunk order everywhere (A/B)
-		const bool rows_on = !getenv("YALM_GEMV_ROWS") || atoi(getenv("YALM_GEMV_ROWS")) != 0;
+		const bool rows_on = !ab_env("YALM_GEMV_ROWS") || atoi(ab_env("YALM_GEMV_ROWS")) != 0;
 		constexpr int W = THREADS / YALM_WAVE;
 		if (rows_on && p.n_groups % nb == 0 && (ngl * P::R) % W == 0 && ngl * P::R >= 2 * W) {
 			auto kern = gemv_rb_kernel<WT, P, U, NORM, THREADS, true>;
@@ -271,11 +271,12 @@ static void launch_attn_D(int G, const float *q, const uint16_t *kc, const uint1
 	// S key-chunk splits per kv head, each workgroup looping over chunks s, s + S, ...: a grid
 	// sized for max_seq_len would issue the speculative first-chunk loads of every idle
 	// workgroup (15.6 MB of dead KV reads per layer at max_seq_len 4096, kv_len ~150).
-	static const int splits = getenv("YALM_ATTN_SPLITS") ? std::max(1, atoi(getenv("YALM_ATTN_SPLITS"))) : 32;
+	static const int splits = ab_env("YALM_ATTN_SPLITS") ? std::max(1, std::min(ATTN_MAX_SPLITS, atoi(ab_env("YALM_ATTN_SPLITS")))) : ATTN_SPLITS;
 	const int nchunks = (max_seq_len + attn_chunk<D>() - 1) / attn_chunk<D>();
-	dim3 grid(n_kv, std::min(nchunks, splits));
+	const int S = std::min(nchunks, splits);
+	const int grid = n_kv * S + n_heads; // attention workgroups, then one merger per query head
 #define YALM_ATTN(GT)                                                                                                  \
-	attn_decode_kernel<D, GT><<<grid, ATTN_THREADS, 0, st>>>(q, kc, vc, step, n_heads, n_kv, max_seq_len, nsplit,    \
+	attn_decode_kernel<D, GT><<<grid, ATTN_THREADS, 0, st>>>(q, kc, vc, step, n_heads, n_kv, max_seq_len, nsplit, S, \
 	                                                         part, layer, n_layers, err, out, att)
 	if (G <= 1)
 		YALM_ATTN(1);
@@ -368,40 +369,24 @@ static int attn_wo_init(yalm_decoder_s *d) {
 		return YALM_OK;
 	const int nchunks = (c.max_seq_len + attn_chunk<128>() - 1) / attn_chunk<128>();
 	// per layer: the attention output as {value, epoch} granules (zero tags never match:
-	// the epoch is >= 1 from the first forward / yalm_block on), then the error word
-	const size_t gran = (size_t)c.n_layers * AWO_GR * c.n_heads * c.head_dim;
+	// the epoch is >= 1 from the first forward / yalm_block on)
+	const size_t gran = (size_t)c.n_layers * c.n_heads * c.head_dim;
 	TRY(dalloc(d, (void **)&d->awo_gran, sizeof(unsigned long long) * gran));
-	// key-chunk splits per kv head, as the standalone attention launch (YALM_AWO_SPLITS: sweep knob)
-	const char *senv = getenv("YALM_AWO_SPLITS");
-	d->awo_S = std::min(nchunks, senv ? std::max(1, atoi(senv)) : 32);
-	d->awo_nb = c.n_kv_heads * d->awo_S + (c.dim + AWO_RPW - 1) / AWO_RPW;
-	// Wo loads in flight per lane (tuning knob): 0 = the whole slice at once, or 8 / 16 / 24
-	const char *wenv = getenv("YALM_ATTN_WO_WIN");
-	const int win = wenv ? atoi(wenv) : 0;
-	if (win != 0 && win != 8 && win != 16 && win != 24) {
-		set_err("YALM_ATTN_WO_WIN must be 0, 8, 16 or 24");
-		return YALM_ERR_ARG;
-	}
-	d->awo_win = d->ablate & 32 ? -1 : win; // ablation bit 32: no Wo weight loads (timing only)
-	const char *denv = getenv("YALM_ATTN_WO_DELAY");
+	// key-chunk splits per kv head, as the standalone attention launch
+	const char *senv = ab_env("YALM_AWO_SPLITS");
+	d->awo_S = std::min(nchunks, senv ? std::max(1, std::min(ATTN_MAX_SPLITS, atoi(senv))) : ATTN_SPLITS);
+	d->awo_nb = c.n_kv_heads * d->awo_S + c.n_heads + (c.dim + AWO_RPW - 1) / AWO_RPW;
+	const char *denv = ab_env("YALM_ATTN_WO_DELAY");
 	// default 0.2 us (fp16) / 0.5 us (fp8): the attention workgroups' K/V loads reach HBM
 	// ahead of the Wo stream. fp16 (33.5 MB, slice lands ~5.4 us, after the heads):
 	// profiles/r2_sweep_awo_delay.txt 10.6 -> 10.1 us at kv_len 17. fp8 (16.8 MB, slice lands
 	// ~3.1 us, before the heads): 0.5 us gives 9.4 -> 8.4 us at kv 17, 11.3 -> 10.3 at kv 151,
 	// 579 -> 586 tok/s (profiles/r3_ab_awo_delay.txt); fp16 at 0.5 us is within noise
 	d->awo_delay = denv ? std::max(0, atoi(denv)) : (c.weight_dtype == YALM_F8E5M2 ? 50 : 20);
-	// combined first attempt (gather + sentinels in one round trip once the slice has
-	// landed, attn_wo.h awo_gather_gran): opt-in, YALM_AWO_SPEC=1. Measured with a fresh
-	// epoch per timed launch it loses (profiles/r3_ab_awo.txt): fp8 kv 17
-	// 9.2 -> 11.0 us, fp16 kv 151 11.2 -> 12.0-12.6; the all-waves gather burst costs more
-	// than the poll round trip it saves
-	const char *spenv = getenv("YALM_AWO_SPEC");
-	d->awo_spec = spenv ? atoi(spenv) != 0 : 0;
-	// copies of the head outputs the Wo workgroups read (one per XCD: the 256 consumers'
-	// gathers spread over 8x the addresses); YALM_AWO_REPL in 1..AWO_GR
-	const char *renv = getenv("YALM_AWO_REPL");
-	d->awo_greps = renv ? std::max(1, std::min(AWO_GR, atoi(renv))) : 1;
-	const char *tenv = getenv("YALM_ATTN_WO_TRACE");
+	// Removed in round 4 (measured losers, round 3, profiles/r3_ab_awo*.txt): the combined
+	// first gather attempt (YALM_AWO_SPEC), per-XCD copies of the head outputs
+	// (YALM_AWO_REPL) and a sliding window on the Wo slice loads (YALM_ATTN_WO_WIN)
+	const char *tenv = ab_env("YALM_ATTN_WO_TRACE");
 	if (tenv && atoi(tenv) != 0)
 		TRY(dalloc(d, (void **)&d->awo_trace, sizeof(unsigned long long) * AWO_TRACE_N * d->awo_nb));
 	d->attn_wo = true;
@@ -472,15 +457,12 @@ static int launch_attn_wo(yalm_decoder_s *d, const yalm_block_weights &w, int la
 	p.part = d->part;
 	p.layer = layer;
 	p.n_layers = c.n_layers;
-	p.gran = d->awo_gran + (size_t)layer * AWO_GR * p.q_dim;
-	p.greps = d->awo_greps;
+	p.gran = d->awo_gran + (size_t)layer * p.q_dim;
 	p.wo = (const char *)w.wo;
 	p.x = d->x;
 	p.err = d->awo_err;
 	p.trace = d->awo_trace;
-	p.win = d->awo_win;
 	p.delay = d->awo_delay;
-	p.spec = d->awo_spec;
 	const int G = c.n_heads / c.n_kv_heads;
 	if constexpr (WT::BYTES == 2 || WT::BYTES == 1) {
 		if (p.q_dim * WT::BYTES == 4096)
@@ -577,8 +559,7 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 	const yalm_block_weights &w = d->b[l];
 	hipStream_t st = d->stream;
 	const int q_dim = c.n_heads * c.head_dim, kv_dim = c.n_kv_heads * c.head_dim;
-	const int ab = d->ablate; // timing-only ablation mask (YALM_ABLATE): results are wrong when set
-	if (!(ab & 1)) {
+	{
 		PQKV<WT> p;
 		p.wq = (const char *)w.wq;
 		p.wk = (const char *)w.wk;
@@ -596,17 +577,14 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 		p.vcache = w.value_cache;
 		TRY((launch_gemv_d<WT, PQKV<WT>, true>(d, p, d->x, w.rms_att, c.norm_eps, GK_QKV)));
 	}
-	if (d->attn_wo && WT::BYTES <= 2 && !(ab & 6)) {
+	if (d->attn_wo && WT::BYTES <= 2) {
 		TRY(launch_attn_wo<WT>(d, w, l));
 	} else {
-		if (!(ab & 2))
-			TRY(launch_attn(c.head_dim, c.n_heads, c.n_kv_heads, d->q, w.key_cache, w.value_cache, d->step,
-			                c.max_seq_len, d->part, l, c.n_layers, d->awo_err, nullptr, d->xb2, st));
-		if (!(ab & 4))
-			TRY(enqueue_residual_gemv<WT>(d, w.wo, q_dim, d->xb2, GK_WO));
+		TRY(launch_attn(c.head_dim, c.n_heads, c.n_kv_heads, d->q, w.key_cache, w.value_cache, d->step, c.max_seq_len,
+		                d->part, l, c.n_layers, d->awo_err, nullptr, d->xb2, st));
+		TRY(enqueue_residual_gemv<WT>(d, w.wo, q_dim, d->xb2, GK_WO));
 	}
-	if (ab & 8) {
-	} else if (c.act == YALM_SILU) {
+	if (c.act == YALM_SILU) {
 		PGlu<WT, 1> p;
 		p.w1 = (const char *)w.w1;
 		p.w3 = (const char *)w.w3;
@@ -623,9 +601,7 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 		p.n_groups = c.hidden_dim;
 		TRY((launch_gemv_d<WT, PGlu<WT, 0>, true>(d, p, d->x, w.rms_ffn, c.norm_eps, GK_GLU)));
 	}
-	if (!(ab & 16))
-		TRY(enqueue_residual_gemv<WT>(d, w.w2, c.hidden_dim, d->hb, GK_W2));
-	return YALM_OK;
+	return enqueue_residual_gemv<WT>(d, w.w2, c.hidden_dim, d->hb, GK_W2);
 }
 
 template <class WT>
@@ -838,10 +814,9 @@ static int create_decoder(const yalm_config *config, const yalm_model_weights *w
 	d->tokens_cap = 1 << 16;
 	d->eager = getenv("YALM_EAGER") && atoi(getenv("YALM_EAGER")) != 0;
 	d->graph_sync = getenv("YALM_GRAPH_SYNC") && atoi(getenv("YALM_GRAPH_SYNC")) != 0;
-	d->ablate = getenv("YALM_ABLATE") ? atoi(getenv("YALM_ABLATE")) : 0;
 	// geometry overrides for A/B runs without a rebuild (same meaning as yalm_set_gemv_config):
 	// YALM_GEMV_CFG="kind:threads:unroll:gpw[,kind:threads:unroll:gpw...]", kind 0..4
-	if (const char *g = getenv("YALM_GEMV_CFG")) {
+	if (const char *g = ab_env("YALM_GEMV_CFG")) {
 		int k, t, u, w, n = 0;
 		for (const char *p = g; sscanf(p, "%d:%d:%d:%d%n", &k, &t, &u, &w, &n) == 4; p += n + (p[n] == ',')) {
 			if (k >= 0 && k < GK_N && (t == 0 || t == 256 || t == 512 || t == 1024) &&
@@ -1217,7 +1192,7 @@ extern "C" int yalm_attn_wo_trace(yalm_decoder d, unsigned long long *host, size
 	if (workgroups)
 		*workgroups = d->awo_nb;
 	if (attention_workgroups)
-		*attention_workgroups = d->c.n_kv_heads * d->awo_S;
+		*attention_workgroups = d->c.n_kv_heads * d->awo_S + d->c.n_heads;
 	return YALM_OK;
 }
 
