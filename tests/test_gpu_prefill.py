@@ -39,23 +39,19 @@ def test_gemm_exact_integers(M_, N, K):
     np.testing.assert_array_equal(c, ref.astype(np.float32))
 
 
-# GEMM forms (yalm_amd/csrc/prefill.h gemm_nt_kernel): LDS-DMA stages 2 / 3 and the
-# 128 x 256 ("wide") tile; read per launch from the environment
-# (the 128-tile forms switch the large-tile kernel off: YALM_PF_G16=0); "g16-256" /
-# "g16-128": prefill_gemm.h gemm16_kernel with 256 x 256 / 256 x 128 tiles everywhere
-# ("g16-256" / "g16-192" / "g16-128" run the 8-phase gemm8p_kernel, "-2ph" the 2-phase
-# gemm16_kernel; "qkv-split": the QKV GEMM as a q launch and a k | v launch from column q_dim)
+# GEMM forms (yalm_amd/csrc/prefill_gemm.h), read when the decoder is created (the
+# yalm_gemm_f16 test hook: per call): "g16-256" / "g16-192" / "g16-128" / "g16-320" force
+# the 256-row tile's width on every GEMM it divides (256 / 192 / 128 run the 8-phase
+# gemm8p_kernel, "-2ph" the 2-phase gemm16_kernel, 320 is always 2-phase); "nopersist":
+# one workgroup per tile instead of the persistent tile loop. The round-2 128 x 128
+# kernel and its stage / wide forms were removed in round 4.
 G16_ALL = "qkv:{0},wo:{0},glu:{0},w2:{0},cls:{0},test:{0}"
-FORMS = {"auto": {}, "s2": {"YALM_PF_STAGES": "2", "YALM_PF_G16": "0"}, "s3": {"YALM_PF_STAGES": "3", "YALM_PF_G16": "0"},
-         "s3-wide": {"YALM_PF_STAGES": "3", "YALM_PF_WIDE": "1", "YALM_PF_G16": "0"},
-         "s2-wide": {"YALM_PF_STAGES": "2", "YALM_PF_WIDE": "1", "YALM_PF_G16": "0"},
-         "s3-narrow": {"YALM_PF_STAGES": "3", "YALM_PF_WIDE": "0", "YALM_PF_G16": "0"},
+FORMS = {"auto": {},
          "g16-256": {"YALM_PF_G16": G16_ALL.format(256)},
          "g16-256-2ph": {"YALM_PF_G16": G16_ALL.format(256), "YALM_PF_8P": "0"}, "g16-128": {"YALM_PF_G16": G16_ALL.format(128)},
          "g16-192": {"YALM_PF_G16": G16_ALL.format(192)},
          "g16-192-2ph": {"YALM_PF_G16": G16_ALL.format(192), "YALM_PF_8P": "0"},
          "g16-128-2ph": {"YALM_PF_G16": G16_ALL.format(128), "YALM_PF_8P": "0"},
-         "qkv-split": {"YALM_PF_QKV_SPLIT": "1"},
          "g16-256-nopersist": {"YALM_PF_G16": G16_ALL.format(256), "YALM_PF_PERSIST": "0"},
          "g16-320": {"YALM_PF_G16": G16_ALL.format(320)}}
 
@@ -65,7 +61,7 @@ FORMS = {"auto": {}, "s2": {"YALM_PF_STAGES": "2", "YALM_PF_G16": "0"}, "s3": {"
                                     (513, 512, 320), (260, 768, 448), (256, 256, 576), (70, 512, 128),
                                     (1100, 16384, 192)])
 def test_gemm_forms_exact(form, M_, N, K, monkeypatch):
-    """Every stage count / tile form is exact on f16-exact integer data (any
+    """Every tile form is exact on f16-exact integer data (any
     staging race or fragment-map error shows as a wrong integer); K tiles 1..10
     (odd and even counts: the 8-phase kernel's iteration covers two K tiles);
     1100 x 16384: more 256 x 256 tiles (320) than CUs, so the persistent tile loop runs."""
@@ -142,11 +138,11 @@ CFGS = {
 
 
 @pytest.mark.parametrize("cfg_name", ["gqa-d128", "d768"])
-@pytest.mark.parametrize("form", ["auto", "s3", "s2-wide", "g16-256", "g16-256-2ph", "g16-128", "g16-128-2ph", "g16-192",
-                                  "g16-192-2ph", "g16-320", "qkv-split", "g16-256-nopersist"])
+@pytest.mark.parametrize("form", ["auto", "g16-256", "g16-256-2ph", "g16-128", "g16-128-2ph", "g16-192",
+                                  "g16-192-2ph", "g16-320", "g16-256-nopersist"])
 def test_prefill_forms_match_decode(form, cfg_name, monkeypatch):
-    """The whole prefill in each GEMM form (the wide tile on every GEMM with N %
-    256 == 0, incl. the vocab-tiled logits epilogue run once per column half)."""
+    """The whole prefill in each GEMM form (incl. the vocab-tiled logits epilogue and
+    the k | v launch at a column offset over the [hi | lo] operand)."""
     for k, v in FORMS[form].items():
         monkeypatch.setenv(k, v)
     cfg = CFGS[cfg_name]

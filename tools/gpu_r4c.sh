@@ -8,6 +8,10 @@ timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method threa
   tests/test_gpu_ref_infer.py tests/test_gpu_kernels.py tests/test_gpu_attn_wo.py tests/test_gpu_mistral_dims.py \
   tests/test_gpu_decode.py > $o/tests.log 2>&1 || { echo "tests failed"; grep -E "FAILED|Error|error" $o/tests.log | head -20; tail -30 $o/tests.log; exit 1; }
 tail -3 $o/tests.log
+timeout -k 10 900 python -u -m pytest -x -v -s --timeout 600 --timeout-method thread \
+  "tests/test_gpu_prefill_llama.py::test_prefill_llama3b_full_depth_vs_oracle" > $o/prefill_depth.log 2>&1
+rc=$?; [ $rc -gt 1 ] && { echo "prefill depth test crashed rc=$rc"; tail -20 $o/prefill_depth.log; exit 1; }
+grep -E "llama-3b dims|passed|failed" $o/prefill_depth.log
 OLD=yalm_amd/ab/libyalm_hip_6ee20fc.so
 NEW=yalm_amd/libyalm_hip.so
 for lib in $OLD $NEW; do

@@ -38,6 +38,7 @@
 #define ATTN_THREADS 256
 #define ATTN_SPLITS 32     // key-chunk splits (workgroups) per kv head
 #define ATTN_MAX_SPLITS 64 // the merger gathers one partial per lane
+#define ATTN_HEAD_MAX 4    // head mode up to this many 64-key chunks (attn_decode_body)
 #define ATTN_WAVES (ATTN_THREADS / YALM_WAVE)
 
 // Keys per workgroup. Small on purpose: one CU streams only ~50-100 GB/s, so
@@ -46,6 +47,13 @@
 template <int D>
 constexpr int attn_chunk() {
 	return 64;
+}
+
+// K / V rows per lane per chunk: lane (row group, piece) covers 8 dims of every
+// (4 waves x 64 / (D / 8))-th row of the chunk
+template <int D>
+constexpr int attn_nk() {
+	return attn_chunk<D>() / (ATTN_WAVES * (64 / (D / 8))) > 0 ? attn_chunk<D>() / (ATTN_WAVES * (64 / (D / 8))) : 1;
 }
 
 __device__ __forceinline__ void st_sc1(float *p, float v) {
@@ -159,13 +167,14 @@ __device__ __forceinline__ float attn_wave_red(float v) {
 	return op(v, xor32(v));
 }
 
-// One workgroup's share of the split-KV attention: kv head g, key chunks s0,
-// s0 + S, ... (S = splits per kv head). With one workgroup holding keys (kv_len <=
-// CHUNK, or S = 1) it writes the normalised head outputs itself and returns true;
-// otherwise it publishes ONE partial per head (unnormalised o[D], max M, sum L) as
-// granules tagged ptag into part [n_heads][nsplit][D + 2] at split s0, and the
-// MERGER workgroups (attn_merge_body, dispatched after every attention workgroup)
-// fold them. D = head_dim (16 .. 256, a power of two); GT >= G.
+// Work of one attention workgroup on kv head g, after its speculative loads (q of
+// the group's G heads in qv, the first chunk's K/V rows in kA / vA): query heads
+// hq0 .. hq0 + Gh - 1 of the group (Gh <= GT) over the key chunks c_first,
+// c_first + cstride, ... < ns. final_out: these are all the keys of those heads --
+// normalise and write the head outputs (returns true); otherwise publish ONE partial
+// per head (unnormalised o[D], max M, sum L) as granules tagged ptag into part
+// [n_heads][nsplit][D + 2] at split s_part, folded by the MERGER workgroups
+// (attn_merge_body). D = head_dim (16 .. 256, a power of two).
 // GRAN: outputs as {value, gtag} granules into `out` read as unsigned long long[].
 // ts / trace_on: attn_wo.h's timeline stamps (thread 0) and the trace-only waits.
 //
@@ -180,26 +189,28 @@ __device__ __forceinline__ float attn_wave_red(float v) {
 // waves. Round 3 published one partial per 64-key chunk and the last attention
 // workgroup merged them in serial batches of 8 (kv 4096: 64 partials, 8 dependent
 // round trips, 20 us standalone).
-template <int D, int GT, bool GRAN>
+template <int D, int GT, int GQ, bool GRAN>
 // (no __restrict__ here: the standalone kernel keeps it on its arguments)
-__device__ __forceinline__ bool attn_decode_body(int g, int s0, int S, const float *q, const uint16_t *kc,
-                                                 const uint16_t *vc, const StepState *step, int n_heads,
-                                                 int n_kv_heads, int max_seq_len, int nsplit, unsigned long long *part,
-                                                 unsigned ptag, unsigned *err, float *out, float *att_dbg,
-                                                 unsigned gtag = 0, unsigned long long *ts = nullptr,
-                                                 bool trace_on = false) {
+__device__ __forceinline__ bool attn_core(int g, int hq0, int Gh, int c_first, int cstride, int ns, bool final_out,
+                                          int s_part, const float4_t (&qv)[(GQ * D + 255) / 256],
+                                          u32x4_t (&kA)[attn_nk<D>()], u32x4_t (&vA)[attn_nk<D>()],
+                                          int kv_len, const uint16_t *kc, const uint16_t *vc, int n_heads,
+                                          int n_kv_heads, int max_seq_len, int nsplit, unsigned long long *part,
+                                          unsigned ptag, float *out, float *att_dbg, unsigned gtag,
+                                          unsigned long long *ts, bool trace_on) {
 	constexpr int CHUNK = attn_chunk<D>();
 	constexpr int LPK = D / 8;                      // lanes per K/V row, 16 B each
 	static_assert(LPK >= 2 && LPK <= 32 && (LPK & (LPK - 1)) == 0, "head_dim 16 .. 256, a power of two");
 	constexpr int KPW = 64 / LPK;                   // row groups per wave (rows per wave-instruction)
 	constexpr int RSTEP = ATTN_WAVES * KPW;         // rows per workgroup-instruction
 	constexpr int NK = CHUNK / RSTEP > 0 ? CHUNK / RSTEP : 1; // rows per lane (D 16: half the rows masked)
-	constexpr int QL = (GT * D + 255) / 256;        // 16-byte q loads per lane (wave-private copy)
-	__shared__ __attribute__((aligned(16))) float qs[ATTN_WAVES][GT * D];
+	constexpr int QL = (GQ * D + 255) / 256;        // 16-byte q loads per lane (wave-private copy)
+	__shared__ __attribute__((aligned(16))) float qs[ATTN_WAVES][GQ * D];
 	__shared__ float wsum[ATTN_WAVES][GT][D]; // per-wave P.V sums
 	__shared__ float wml[ATTN_WAVES][GT][2];  // per-wave (max, sum of exp)
 
 	const int G = n_heads / n_kv_heads;
+	const int hb = g * G + hq0; // first query head computed here
 	const int kv_dim = n_kv_heads * D;
 	const int lane = threadIdx.x & 63;
 	const int wave = threadIdx.x >> 6;
@@ -217,16 +228,6 @@ __device__ __forceinline__ bool attn_decode_body(int g, int s0, int S, const flo
 			vw[i] = load16(vc + off);
 		}
 	};
-	// ---- speculative loads: q of the group's G heads (G * D contiguous floats, QL
-	// 16-byte pieces per lane), the first chunk's K/V rows (clamped to the cache), step
-	const int gq = G * D;
-	float4_t qv[QL];
-#pragma unroll
-	for (int j = 0; j < QL; ++j)
-		qv[j] = *(const float4_t *)(q + (size_t)g * gq + min((j * 64 + lane) * 4, gq - 4));
-	u32x4_t kA[NK], vA[NK];
-	load_kv(s0 * CHUNK, max_seq_len - 1, kA, vA);
-	const int kv_len = step->kv_len;
 	// trace (attn_wo.h, thread 0 only): s_memrealtime + shader clock (s_memtime) at
 	// checkpoint k, kept in registers and stored at the end -- a store issued mid-way
 	// would queue behind the co-resident Wo workgroup's weight loads and stall the wave
@@ -245,10 +246,6 @@ __device__ __forceinline__ bool attn_decode_body(int g, int s0, int S, const flo
 					ts[k] = tsr[k], ts[8 + k] = tsc[k];
 		}
 	};
-	if (s0 * CHUNK >= kv_len) {
-		flush();
-		return false; // whole workgroup leaves before any barrier
-	}
 	if (trace_on) { // tracing only: when the first chunk's loads have landed in every wave
 		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 		__syncthreads();
@@ -256,6 +253,7 @@ __device__ __forceinline__ bool attn_decode_body(int g, int s0, int S, const flo
 	}
 	// q through this wave's own LDS copy: lane (row group, piece) needs dims piece*8..+8
 	// of every head (LDS reads from one wave are ordered after its writes: no barrier)
+	const int gq = G * D;
 #pragma unroll
 	for (int j = 0; j < QL; ++j)
 		if ((j * 64 + lane) * 4 < gq)
@@ -263,14 +261,12 @@ __device__ __forceinline__ bool attn_decode_body(int g, int s0, int S, const flo
 	float qr[GT][8];
 #pragma unroll
 	for (int h = 0; h < GT; ++h) {
-		const float *qp = &qs[wave][(h < G ? h : 0) * D + piece * 8];
+		const float *qp = &qs[wave][(hq0 + (h < Gh ? h : 0)) * D + piece * 8];
 		const float4_t a = *(const float4_t *)qp;
 		const float4_t b = *(const float4_t *)(qp + 4);
 		qr[h][0] = a[0], qr[h][1] = a[1], qr[h][2] = a[2], qr[h][3] = a[3];
 		qr[h][4] = b[0], qr[h][5] = b[1], qr[h][6] = b[2], qr[h][7] = b[3];
 	}
-	const int ns = (kv_len + CHUNK - 1) / CHUNK;
-	const int nact = min(ns, S); // workgroups of kv head g with keys: one partial each
 	const float sq = sqrtf((float)D);
 
 	// running state of this wave over its chunks: P.V sums (element e of head h at dim
@@ -327,8 +323,8 @@ __device__ __forceinline__ bool attn_decode_body(int g, int s0, int S, const flo
 				ok[j] = f < V && tl0 + i * RSTEP < nt;
 				sc[j] = sc[j] / sq;
 				m = ok[j] ? fmaxf(m, sc[j]) : m;
-				if (att_dbg && ok[j] && h < G) // test hook: raw scores (normalised by the writer)
-					st_sc1(att_dbg + (size_t)(g * G + h) * max_seq_len + t0 + tl0 + i * RSTEP, sc[j]);
+				if (att_dbg && ok[j] && h < Gh) // test hook: raw scores (normalised by the writer)
+					st_sc1(att_dbg + (size_t)(hb + h) * max_seq_len + t0 + tl0 + i * RSTEP, sc[j]);
 			}
 			stamp(4);
 			// ---- per-wave softmax statistics of head h over the row's lanes of the same
@@ -439,37 +435,37 @@ __device__ __forceinline__ bool attn_decode_body(int g, int s0, int S, const flo
 		}
 	};
 
-	// chunks s0, s0 + S, ...: one chunk per workgroup up to kv_len S * CHUNK (straight-line
-	// loads); beyond it the next chunk's rows are loaded before the current one is computed
-	// (the prefetch past the last chunk re-reads row kv_len - 1: unconditional loads keep
-	// hipcc's vmcnt counting exact, a conditional one would drain to 0 before every load)
+	// chunks c_first, c_first + cstride, ...: straight-line loads for one chunk; beyond
+	// it the next chunk's rows are loaded before the current one is computed (the prefetch
+	// past the last chunk re-reads row kv_len - 1: unconditional loads keep hipcc's vmcnt
+	// counting exact, a conditional one would drain to 0 before every load)
 	using T_ = std::true_type;
 	using F_ = std::false_type;
-	if (s0 + S >= ns) {
-		chunk(T_{}, kA, vA, s0 * CHUNK);
+	if (c_first + cstride >= ns) {
+		chunk(T_{}, kA, vA, c_first * CHUNK);
 	} else {
 		u32x4_t kB[NK], vB[NK];
-		load_kv((s0 + S) * CHUNK, kv_len - 1, kB, vB);
-		chunk(T_{}, kA, vA, s0 * CHUNK);
-		for (int c = s0 + S;; c += 2 * S) { // kB / vB hold chunk c
-			load_kv((c + S) * CHUNK, kv_len - 1, kA, vA);
+		load_kv((c_first + cstride) * CHUNK, kv_len - 1, kB, vB);
+		chunk(T_{}, kA, vA, c_first * CHUNK);
+		for (int c = c_first + cstride;; c += 2 * cstride) { // kB / vB hold chunk c
+			load_kv((c + cstride) * CHUNK, kv_len - 1, kA, vA);
 			chunk(F_{}, kB, vB, c * CHUNK);
-			if (c + S >= ns)
+			if (c + cstride >= ns)
 				break;
-			load_kv((c + 2 * S) * CHUNK, kv_len - 1, kB, vB);
-			chunk(F_{}, kA, vA, (c + S) * CHUNK);
-			if (c + 2 * S >= ns)
+			load_kv((c + 2 * cstride) * CHUNK, kv_len - 1, kB, vB);
+			chunk(F_{}, kA, vA, (c + cstride) * CHUNK);
+			if (c + 2 * cstride >= ns)
 				break;
 		}
 	}
 
 	// ---- this wave's running (max, sum) and P.V sums over its row groups, into LDS
 	if constexpr (LPK == 16) {
-		if (lane < GT && lane < G) {
+		if (lane < GT && lane < Gh) {
 			wml[wave][lane][0] = Mr;
 			wml[wave][lane][1] = Lr;
 		}
-	} else if (lane < G) {
+	} else if (lane < Gh) {
 		float m = mw[0], l = lw[0];
 #pragma unroll
 		for (int h = 1; h < GT; ++h)
@@ -490,7 +486,7 @@ __device__ __forceinline__ bool attn_decode_body(int g, int s0, int S, const flo
 			const float v4[4] = {acc[4 * k], acc[4 * k + 1], acc[4 * k + 2], acc[4 * k + 3]};
 			const float s = sum4_rows(v4);
 			const int idx = 4 * k + (lane >> 4), h = idx >> 3, e = idx & 7;
-			if (h < G && (lane & 15) < LPK)
+			if (h < Gh && (lane & 15) < LPK)
 				wsum[wave][h][(lane & 15) * 8 + e] = s;
 		}
 	} else { // LPK 32: two row groups, the wave's halves
@@ -502,7 +498,7 @@ __device__ __forceinline__ bool attn_decode_body(int g, int s0, int S, const flo
 			for (int h = 0; h < GT; ++h)
 #pragma unroll
 				for (int e = 0; e < 8; ++e)
-					if (h < G)
+					if (h < Gh)
 						wsum[wave][h][lane * 8 + e] = acc[h * 8 + e];
 		}
 	}
@@ -512,7 +508,7 @@ __device__ __forceinline__ bool attn_decode_body(int g, int s0, int S, const flo
 	stamp(6);
 
 	// ---- combine the waves (fixed order): o = sum_w e^(m_w - M) o_w, L likewise
-	for (int i = tid; i < G * D; i += ATTN_THREADS) {
+	for (int i = tid; i < Gh * D; i += ATTN_THREADS) {
 		const int h = i / D, d = i % D;
 		float M = wml[0][h][0];
 #pragma unroll
@@ -525,10 +521,10 @@ __device__ __forceinline__ bool attn_decode_body(int g, int s0, int S, const flo
 			o = fmaf(wsum[w][h][d], c, o);
 			L = fmaf(wml[w][h][1], c, L);
 		}
-		if (nact == 1) { // the only workgroup with keys: normalise and write the head outputs
-			attn_out<GRAN>(out, (size_t)(g * G + h) * D + d, o / L, gtag);
+		if (final_out) { // all keys of these heads: normalise and write the head outputs
+			attn_out<GRAN>(out, (size_t)(hb + h) * D + d, o / L, gtag);
 		} else { // this workgroup's partial (o[D], M, L per head) as tagged granules
-			const size_t pp = ((size_t)(g * G + h) * nsplit + s0) * (D + 2);
+			const size_t pp = ((size_t)(hb + h) * nsplit + s_part) * (D + 2);
 			attn_out<true>((float *)part, pp + d, o, ptag);
 			if (d == 0) {
 				attn_out<true>((float *)part, pp + D, M, ptag);
@@ -536,9 +532,9 @@ __device__ __forceinline__ bool attn_decode_body(int g, int s0, int S, const flo
 			}
 		}
 	}
-	if (nact == 1 && att_dbg) { // test hook: raw scores -> probabilities
+	if (final_out && att_dbg) { // test hook: raw scores -> probabilities
 		const int nt = kv_len;
-		for (int i = tid; i < G * nt; i += ATTN_THREADS) {
+		for (int i = tid; i < Gh * nt; i += ATTN_THREADS) {
 			const int h = i / nt, t = i % nt;
 			float M = wml[0][h][0];
 #pragma unroll
@@ -548,16 +544,81 @@ __device__ __forceinline__ bool attn_decode_body(int g, int s0, int S, const flo
 #pragma unroll
 			for (int w = 0; w < ATTN_WAVES; ++w)
 				L = fmaf(wml[w][h][1], expf(wml[w][h][0] - M), L);
-			float *a = att_dbg + (size_t)(g * G + h) * max_seq_len + t;
+			float *a = att_dbg + (size_t)(hb + h) * max_seq_len + t;
 			*a = expf(ld_sc1(a) - M) / L;
 		}
 	}
 	flush();
-	return nact == 1;
+	return final_out;
 }
 
-// MERGER workgroup of (kv head g, query head h = g * G + hq): with nact > 1
-// attention workgroups holding keys, gathers their nact partials of head h and
+// One attention workgroup (kv head g, split s0 of S): speculative loads, then one of
+//   * HEAD mode (kv_len <= head_max chunks; workgroups s0 < G): query head s0 of the
+//     group over ALL the chunks, written directly -- no partial, no merger hop, and a
+//     quarter of the per-wave arithmetic of a 4-head chunk (Mistral: G = 4). The G
+//     workgroups of a kv head read the same K/V rows (the 2nd .. Gth from L2).
+//   * KEY mode (longer contexts): every query head of the group over chunks s0,
+//     s0 + S, ...: one partial per head for the mergers (or, with one workgroup holding
+//     keys, the head outputs).
+// The speculative first-chunk rows are chunk 0 for s0 < G (head mode's) and chunk s0
+// otherwise; a key-mode workgroup 0 < s0 < G re-issues its own.
+// Returns true on a workgroup that wrote head outputs.
+template <int D, int GT, bool GRAN>
+__device__ __forceinline__ bool attn_decode_body(int g, int s0, int S, int head_max, const float *q,
+                                                 const uint16_t *kc, const uint16_t *vc, const StepState *step,
+                                                 int n_heads, int n_kv_heads, int max_seq_len, int nsplit,
+                                                 unsigned long long *part, unsigned ptag, float *out, float *att_dbg,
+                                                 unsigned gtag = 0, unsigned long long *ts = nullptr,
+                                                 bool trace_on = false) {
+	constexpr int CHUNK = attn_chunk<D>();
+	constexpr int LPK = D / 8;
+	constexpr int KPW = 64 / LPK;
+	constexpr int RSTEP = ATTN_WAVES * KPW;
+	constexpr int NK = CHUNK / RSTEP > 0 ? CHUNK / RSTEP : 1;
+	constexpr int QL = (GT * D + 255) / 256;
+	const int G = n_heads / n_kv_heads;
+	const int kv_dim = n_kv_heads * D;
+	const int lane = threadIdx.x & 63;
+	const int tl0 = (threadIdx.x >> 6) * KPW + lane / LPK;
+	const int piece = lane % LPK;
+	auto load_kv = [&](int t0, u32x4_t (&kw)[NK], u32x4_t (&vw)[NK]) {
+#pragma unroll
+		for (int i = 0; i < NK; ++i) {
+			const int t = min(t0 + tl0 + i * RSTEP, max_seq_len - 1);
+			const size_t off = (size_t)t * kv_dim + g * D + piece * 8;
+			kw[i] = load16(kc + off);
+			vw[i] = load16(vc + off);
+		}
+	};
+	// ---- speculative loads: q of the group's G heads (G * D contiguous floats, QL
+	// 16-byte pieces per lane), a first chunk's K/V rows (clamped to the cache), step
+	const int gq = G * D;
+	float4_t qv[QL];
+#pragma unroll
+	for (int j = 0; j < QL; ++j)
+		qv[j] = *(const float4_t *)(q + (size_t)g * gq + min((j * 64 + lane) * 4, gq - 4));
+	const bool hcand = s0 < G;
+	u32x4_t kA[NK], vA[NK];
+	load_kv((hcand ? 0 : s0) * CHUNK, kA, vA);
+	const int kv_len = step->kv_len;
+	const int ns = (kv_len + CHUNK - 1) / CHUNK;
+	if (ns <= head_max) {
+		if (!hcand)
+			return false; // whole workgroup leaves before any barrier
+		return attn_core<D, 1, GT, GRAN>(g, s0, 1, 0, 1, ns, true, 0, qv, kA, vA, kv_len, kc, vc, n_heads, n_kv_heads,
+		                                 max_seq_len, nsplit, part, ptag, out, att_dbg, gtag, ts, trace_on);
+	}
+	if (s0 * CHUNK >= kv_len)
+		return false;
+	if (hcand && s0 != 0)
+		load_kv(s0 * CHUNK, kA, vA);
+	const int nact = min(ns, S); // workgroups of kv head g with keys: one partial each
+	return attn_core<D, GT, GT, GRAN>(g, 0, G, s0, S, ns, nact == 1, s0, qv, kA, vA, kv_len, kc, vc, n_heads,
+	                                  n_kv_heads, max_seq_len, nsplit, part, ptag, out, att_dbg, gtag, ts, trace_on);
+}
+
+// MERGER workgroup of (kv head g, query head h = g * G + hq): in key mode with
+// nact > 1 attention workgroups holding keys, gathers their nact partials of head h and
 // writes the normalised head output. Mergers are dispatched after every attention
 // workgroup of the launch, so they only wait on earlier ones (no deadlock however
 // few workgroups are resident). Wave w takes splits w, w + 4, ...: all its granule
@@ -568,7 +629,7 @@ __device__ __forceinline__ bool attn_decode_body(int g, int s0, int S, const flo
 // the round-4 first cut merged all G heads of a kv head in ONE workgroup (131 KB
 // through one CU). Returns true if it wrote the head (nact > 1).
 template <int D, bool GRAN>
-__device__ __forceinline__ bool attn_merge_body(int g, int hq, int S, const StepState *step, int n_heads,
+__device__ __forceinline__ bool attn_merge_body(int g, int hq, int S, int head_max, const StepState *step, int n_heads,
                                                 int n_kv_heads, int max_seq_len, int nsplit,
                                                 const unsigned long long *part, unsigned ptag, unsigned *err,
                                                 float *out, float *att_dbg, unsigned gtag = 0) {
@@ -582,8 +643,8 @@ __device__ __forceinline__ bool attn_merge_body(int g, int hq, int S, const Step
 	const int kv_len = step->kv_len;
 	const int ns = (kv_len + CHUNK - 1) / CHUNK;
 	const int nact = min(ns, S);
-	if (nact <= 1 || hq >= G)
-		return false;
+	if (ns <= head_max || nact <= 1 || hq >= G)
+		return false; // head mode, or one workgroup held every key: nothing to merge
 	const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
 	const int nsw = (nact - wave + ATTN_WAVES - 1) / ATTN_WAVES; // this wave's splits: wave + 4 j, j < nsw
 	const int dl = lane < D ? lane : 0; // lanes past D (D < 64) re-read dim 0 and only follow along
@@ -678,14 +739,14 @@ template <int D, int GT>
 __global__ __launch_bounds__(ATTN_THREADS) void attn_decode_kernel(
     const float *__restrict__ q, const uint16_t *__restrict__ kc, const uint16_t *__restrict__ vc,
     const StepState *__restrict__ step, int n_heads, int n_kv_heads, int max_seq_len, int nsplit, int S,
-    unsigned long long *__restrict__ part, int layer, int n_layers, unsigned *__restrict__ err,
+    int head_max, unsigned long long *__restrict__ part, int layer, int n_layers, unsigned *__restrict__ err,
     float *__restrict__ out, float *__restrict__ att_dbg) {
 	const int b = blockIdx.x, units = n_kv_heads * S;
 	const unsigned ptag = attn_part_tag(step, layer, n_layers);
 	if (b < units)
-		attn_decode_body<D, GT, false>(b % n_kv_heads, b / n_kv_heads, S, q, kc, vc, step, n_heads, n_kv_heads,
-		                               max_seq_len, nsplit, part, ptag, err, out, att_dbg);
+		attn_decode_body<D, GT, false>(b % n_kv_heads, b / n_kv_heads, S, head_max, q, kc, vc, step, n_heads,
+		                               n_kv_heads, max_seq_len, nsplit, part, ptag, out, att_dbg);
 	else
-		attn_merge_body<D, false>((b - units) % n_kv_heads, (b - units) / n_kv_heads, S, step, n_heads, n_kv_heads,
-		                          max_seq_len, nsplit, part, ptag, err, out, att_dbg);
+		attn_merge_body<D, false>((b - units) % n_kv_heads, (b - units) / n_kv_heads, S, head_max, step, n_heads,
+		                          n_kv_heads, max_seq_len, nsplit, part, ptag, err, out, att_dbg);
 }

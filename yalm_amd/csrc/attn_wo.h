@@ -47,6 +47,7 @@
 
 struct AttnWoArgs {
 	int n_heads, n_kv, max_seq_len, nsplit, S; // S = key-chunk splits per kv head: n_kv * S attention workgroups
+	int head_max;                              // head mode up to this many 64-key chunks (attention.h)
 	int q_dim, dim;
 	unsigned long long *part; // attention chunk partials (n_heads, nsplit, D + 2) as tagged granules
 	int layer, n_layers;      // partial tag = epoch * n_layers + layer (attention.h)
@@ -185,11 +186,11 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 	if (b < munits) { // ---- attention or merger workgroup
 		const unsigned ptag = epoch * (unsigned)p.n_layers + (unsigned)p.layer;
 		const bool wrote =
-		    b < units ? attn_decode_body<D, GT, true>(b % p.n_kv, b / p.n_kv, p.S, q, kc, vc, step, p.n_heads, p.n_kv,
-		                                               p.max_seq_len, p.nsplit, p.part, ptag, p.err, (float *)p.gran,
-		                                               nullptr, epoch, tr, p.trace != nullptr)
-		              : attn_merge_body<D, true>((b - units) % p.n_kv, (b - units) / p.n_kv, p.S, step, p.n_heads,
-		                                         p.n_kv, p.max_seq_len, p.nsplit, p.part, ptag, p.err,
+		    b < units ? attn_decode_body<D, GT, true>(b % p.n_kv, b / p.n_kv, p.S, p.head_max, q, kc, vc, step,
+		                                               p.n_heads, p.n_kv, p.max_seq_len, p.nsplit, p.part, ptag,
+		                                               (float *)p.gran, nullptr, epoch, tr, p.trace != nullptr)
+		              : attn_merge_body<D, true>((b - units) % p.n_kv, (b - units) / p.n_kv, p.S, p.head_max, step,
+		                                         p.n_heads, p.n_kv, p.max_seq_len, p.nsplit, p.part, ptag, p.err,
 		                                         (float *)p.gran, nullptr, epoch);
 		if (tr) { // the head outputs are their own ready flags: nothing to drain or signal
 			const unsigned long long t1 = __builtin_amdgcn_s_memrealtime(), c1 = __builtin_amdgcn_s_memtime();

@@ -66,7 +66,7 @@ inline const char *ab_env(const char *name) {
 struct PrefillBufs {
 	int cap = 0;
 	float *X = nullptr;        // [cap][dim] f32 residual stream
-	uint16_t *Xn = nullptr;    // [cap][dim] f16 normalised A operand
+	uint16_t *Xn = nullptr;    // [cap][2 dim] f16 normalised A operand ([hi | lo] before the QKV GEMM)
 	uint16_t *Q = nullptr;     // [cap][q_dim] f16
 	uint16_t *O = nullptr;     // [cap][q_dim] f16 attention output
 	uint16_t *H = nullptr;     // [cap][hidden] f16 GLU output
@@ -76,6 +76,16 @@ struct PrefillBufs {
 	float *tgt_logit = nullptr, *lp = nullptr; // [cap]
 	float *rope = nullptr;                     // [cap][head_dim / 2][2]
 };
+
+// Prefill GEMM forms (prefill.hip): per GEMM kind the large-tile width (-1 = auto,
+// 128 / 192 / 256 / 320), the 8-phase schedule, the persistent tile loop. Fixed at
+// decoder creation (YALM_PF_G16 / YALM_PF_8P / YALM_PF_PERSIST select other exact forms
+// for the tests); never re-read per launch.
+struct PfForms {
+	int g16[6] = {-1, -1, -1, -1, -1, -1}; // qkv, wo, glu, w2, cls, test
+	bool p8 = true, persist = true;
+};
+PfForms pf_forms_from_env();
 
 // ------------------------------------------------------------------ decoder
 enum { GRAPH_HYDRATE = 0, GRAPH_LOGITS = 1, GRAPH_GREEDY = 2, N_GRAPHS = 3 };
@@ -103,6 +113,7 @@ struct yalm_decoder_s {
 	bool graph_sync = false; // YALM_GRAPH_SYNC=1: synchronise after every replay
 	std::string kname;
 	PrefillBufs pf;
+	PfForms pf_forms;
 	// tensor parallelism (yalm_decoder_create_tp): c holds the LOCAL shard dims
 	// (n_heads, n_kv_heads, hidden_dim, vocab_size divided by tp_size)
 	int tp_rank = 0, tp_size = 1;

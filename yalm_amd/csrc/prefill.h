@@ -15,9 +15,11 @@
 //   logits = f16(rmsnorm(X)) · Wcls^T -> per-row (max, sum exp, target logit)
 // Weights stay in the .yalm layout ([out][in] f16, row-major): C = A · W^T is
 // an "NT" GEMM whose two operands are both K-contiguous, so every MFMA operand
-// fragment is a 16-byte row read (no transposes). Accumulation is f32; the
-// activations are rounded to f16 for the MFMA inputs (the parity tolerance of
-// tests/test_gpu_prefill.py covers exactly that).
+// fragment is a 16-byte row read (no transposes); the GEMMs are in
+// prefill_gemm.h. Accumulation is f32; the activations are rounded to f16 for
+// the MFMA inputs, except the K / V columns of the QKV GEMM, whose A operand is
+// the normalised x split as f16 hi + lo (round 4: the K / V cache rows then carry
+// one f16 rounding, as infer.cpp:299's, not two).
 #pragma once
 
 #include <float.h>
@@ -29,9 +31,8 @@ typedef float f32x16_t __attribute__((ext_vector_type(16)));
 
 namespace pf {
 
-constexpr int BM = 128, BN = 128, BK = 64; // block tile; BK = 64 f16 = 128-byte rows
-constexpr int THREADS = 256;               // 4 waves as 2 (M) x 2 (N), 64 x 64 each
-constexpr int TILE = BM * BK;              // f16 elements per staged operand tile (16 KB)
+constexpr int BN = 128, BK = 64; // prefill dims must be multiples of BN (and of BK for K)
+constexpr int THREADS = 256;      // attention prefill: 4 waves x 32 queries
 
 __device__ __forceinline__ uint16_t f2h_bits(float x) {
 	_Float16 h = (_Float16)x;
@@ -40,199 +41,8 @@ __device__ __forceinline__ uint16_t f2h_bits(float x) {
 	return u;
 }
 
-// Stage a 128-row x 64-k f16 tile global -> LDS with 16-byte LDS-DMA
-// (global_load_lds_dwordx4): wave-instruction = 1 KB = 8 rows. The LDS image
-// is lane-linear; the XOR swizzle (chunk ^ (row & 7)) goes on the per-lane
-// SOURCE address, the matching read is frag_addr below. Rows past `rows`
-// re-read the last valid row (never stored).
-__device__ __forceinline__ void stage_tile(uint16_t *lds_tile, const uint16_t *__restrict__ g, int ld, int row0,
-                                           int rows, int k0, int wave, int lane) {
-#pragma unroll
-	for (int i = 0; i < BM / 8 / (THREADS / 64); ++i) {
-		const int rb = wave * (BM / 8 / (THREADS / 64)) + i;
-		const int r = rb * 8 + (lane >> 3);
-		const int c = lane & 7;
-		const int gr = min(row0 + r, rows - 1);
-		const uint16_t *src = g + (size_t)gr * ld + k0 + 8 * (c ^ (r & 7));
-		__builtin_amdgcn_global_load_lds((const void *)src, (YALM_LDS void *)(lds_tile + rb * 8 * BK), 16, 0, 0);
-	}
-}
-
-// 32x32x16 f16 operand fragment of tile row r, k-step s (16 deep): lane half h
-// holds k = 16 s + 8 h .. +7 (cdna_hip_programming.md §3 A/B lane maps).
-__device__ __forceinline__ half8_t frag(const uint16_t *lds_tile, int r, int s, int h) {
-	const int kc = 2 * s + h;
-	return *(const half8_t *)(lds_tile + r * BK + 8 * (kc ^ (r & 7)));
-}
-
 // C/D map of v_mfma_f32_32x32x16: column = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5).
 __device__ __forceinline__ int crow(int reg, int lane) { return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); }
-
-// ---------------------------------------------------------------- epilogues
-// Each gets the wave's accumulators acc[NB][2][2] (32x32 tiles, rows m0 + 32 i,
-// columns n0 + 32 j) after the K loop.
-
-struct EpiStoreF32 { // C -> f32 (tests)
-	static constexpr bool NEEDS_LDS = false;
-	float *red = nullptr;
-	float *c;
-	int ldc, M;
-	template <int NB>
-	__device__ __forceinline__ void apply(f32x16_t (&acc)[NB][2][2], int m0, int n0, int lane) const {
-#pragma unroll
-		for (int i = 0; i < 2; ++i)
-#pragma unroll
-			for (int j = 0; j < 2; ++j)
-#pragma unroll
-				for (int r = 0; r < 16; ++r) {
-					const int m = m0 + 32 * i + crow(r, lane), n = n0 + 32 * j + (lane & 31);
-					if (m < M)
-						c[(size_t)m * ldc + n] = acc[0][i][j][r];
-				}
-	}
-};
-
-struct EpiResidual { // X[m][n] += C  (fused_matmul_add_residuals, per row)
-	static constexpr bool NEEDS_LDS = false;
-	float *red = nullptr;
-	float *x;
-	int ldx, M;
-	template <int NB>
-	__device__ __forceinline__ void apply(f32x16_t (&acc)[NB][2][2], int m0, int n0, int lane) const {
-#pragma unroll
-		for (int i = 0; i < 2; ++i)
-#pragma unroll
-			for (int j = 0; j < 2; ++j)
-#pragma unroll
-				for (int r = 0; r < 16; ++r) {
-					const int m = m0 + 32 * i + crow(r, lane), n = n0 + 32 * j + (lane & 31);
-					if (m < M)
-						x[(size_t)m * ldx + n] += acc[0][i][j][r];
-				}
-	}
-};
-
-template <int ACT>
-struct EpiGlu { // H = f16(act(X W1^T) * (X W3^T))  (fused_ffn_w1_w3_glu_act)
-	static constexpr bool NEEDS_LDS = false;
-	float *red = nullptr;
-	uint16_t *h;
-	int ldh, M;
-	template <int NB>
-	__device__ __forceinline__ void apply(f32x16_t (&acc)[NB][2][2], int m0, int n0, int lane) const {
-#pragma unroll
-		for (int i = 0; i < 2; ++i)
-#pragma unroll
-			for (int j = 0; j < 2; ++j)
-#pragma unroll
-				for (int r = 0; r < 16; ++r) {
-					const int m = m0 + 32 * i + crow(r, lane), n = n0 + 32 * j + (lane & 31);
-					if (m < M)
-						h[(size_t)m * ldh + n] = f2h_bits(act_fn<ACT>(acc[0][i][j][r]) * acc[NB - 1][i][j][r]);
-				}
-	}
-};
-
-// [q | k | v] columns: clip (infer.cpp:280-288), RoPE on (even, odd) column
-// pairs = lanes (l, l ^ 1) via DPP (infer.cpp:291-301, angle = pos * freq),
-// q -> f16 Q[T][q_dim], k / v -> the fp16 KV cache rows pos0 + m
-// (fused_rope_and_cache_update, infer.cu:642-677).
-struct EpiQKV {
-	static constexpr bool NEEDS_LDS = false;
-	float *red = nullptr;
-	uint16_t *q;
-	uint16_t *kc, *vc;
-	const float *rope; // [M][head_dim / 2][2] (cos, sin) of pos * inv_freq (rope_table_kernel)
-	int M, q_dim, kv_dim, head_dim, pos0;
-	float clip;
-	template <int NB>
-	__device__ __forceinline__ void apply(f32x16_t (&acc)[NB][2][2], int m0, int n0, int lane) const {
-		const bool odd = lane & 1;
-#pragma unroll
-		for (int i = 0; i < 2; ++i)
-#pragma unroll
-			for (int j = 0; j < 2; ++j) {
-				const int n = n0 + 32 * j + (lane & 31);
-				const bool is_v = n >= q_dim + kv_dim;
-				const int nn = n < q_dim ? n : (n < q_dim + kv_dim ? n - q_dim : n - q_dim - kv_dim);
-				const int fj = (nn % head_dim) >> 1;
-#pragma unroll
-				for (int r = 0; r < 16; ++r) {
-					float v = acc[0][i][j][r];
-					v = v < -clip ? -clip : (v > clip ? clip : v);
-					const float p = dpp<0xB1>(v); // partner column (n ^ 1)
-					const int m = m0 + 32 * i + crow(r, lane);
-					if (m >= M)
-						continue;
-					const int pos = pos0 + m;
-					float o = v;
-					if (!is_v) {
-						const float2_t cs = *(const float2_t *)(rope + ((size_t)m * (head_dim >> 1) + fj) * 2);
-						o = odd ? p * cs[1] + v * cs[0] : v * cs[0] - p * cs[1];
-					}
-					if (n < q_dim)
-						q[(size_t)m * q_dim + n] = f2h_bits(o);
-					else if (!is_v)
-						kc[(size_t)pos * kv_dim + nn] = f2h(o);
-					else
-						vc[(size_t)pos * kv_dim + nn] = f2h(o);
-				}
-			}
-	}
-};
-
-// Per (row, 128-column tile): max and sum of exp over the tile's logits, and
-// the target token's logit when it falls in the tile (sample_prob,
-// sampler.cpp:11-25, split over vocab tiles; combined by logprob_kernel).
-struct EpiLogits {
-	static constexpr bool NEEDS_LDS = true;
-	float *pmax, *psum, *tgt_logit;
-	const int *targets; // target token of row m (-1: none)
-	int M, ntiles;
-	float *red; // LDS scratch [2 waves (N)][128 rows][2]
-	template <int NB>
-	__device__ __forceinline__ void apply(f32x16_t (&acc)[NB][2][2], int m0, int n0, int lane) const {
-		const int wave = threadIdx.x >> 6;
-		const int wn = wave & 1, wm = wave >> 1;
-#pragma unroll
-		for (int i = 0; i < 2; ++i) {
-#pragma unroll
-			for (int r = 0; r < 16; ++r) {
-				const int ml = 32 * i + crow(r, lane); // row within the wave's 64
-				const int m = m0 + ml;
-				const int tgt = m < M ? targets[m] : -1;
-				float mx = fmaxf(acc[0][i][0][r], acc[0][i][1][r]);
-				mx = row16_max(mx);
-				mx = fmaxf(mx, xor16(mx)); // 32 columns of this lane half
-#pragma unroll
-				for (int j = 0; j < 2; ++j) {
-					const int n = n0 + 32 * j + (lane & 31);
-					if (n == tgt)
-						tgt_logit[m] = acc[0][i][j][r];
-				}
-				float s = expf(acc[0][i][0][r] - mx) + expf(acc[0][i][1][r] - mx);
-				s = row16_sum(s);
-				s += xor16(s);
-				if ((lane & 31) == 0) {
-					red[(wn * BM + wm * 64 + ml) * 2 + 0] = mx;
-					red[(wn * BM + wm * 64 + ml) * 2 + 1] = s;
-				}
-			}
-		}
-		__syncthreads();
-		for (int row = threadIdx.x; row < BM; row += THREADS) {
-			const int m = m0 - (m0 % BM) + row; // block's row
-			if (m >= M)
-				continue;
-			const float a = red[row * 2], sa = red[row * 2 + 1];
-			const float b = red[(BM + row) * 2], sb = red[(BM + row) * 2 + 1];
-			const float mx = fmaxf(a, b);
-			const int tile = (n0 - (n0 % BN)) / BN;
-			pmax[(size_t)m * ntiles + tile] = mx;
-			psum[(size_t)m * ntiles + tile] = sa * expf(a - mx) + sb * expf(b - mx);
-		}
-	}
-};
 
 // B operand rows n = 0..N-1 drawn from up to 3 row-major [rows][K] matrices
 // laid end to end (wq | wk | wv). Every 128-row tile lies inside one segment.
@@ -248,146 +58,8 @@ struct BSrc {
 	}
 };
 
-// C[M, N] (epilogue) = A[M, K] · W_b[N, K]^T for b < NB (NB = 2: W1 and W3
-// share the A tile). N % 128 == 0, K % 64 == 0, any M.
-//   NS = 2: two LDS buffers; the next K tile's LDS-DMA is issued before the
-//     current tile's MFMAs and drained (vmcnt(0) + barrier) after them (the
-//     2-phase structure of cdna_hip_programming.md §5.5 T3+T4, minimum form).
-//   NS = 3: three LDS buffers, ONE tile kept in flight across every barrier
-//     (cdna_hip_programming.md §5 "Pipelining across barriers": counted
-//     vmcnt(N) — N = this thread's LDS-DMA instructions per tile — and a raw
-//     s_barrier with lgkmcnt(0) only; __syncthreads() would drain the DMA).
-//     Per K step: wait for tile kt (tile kt + 1 may stay in flight) -> barrier
-//     (every wave's tile kt landed; every wave done reading tile kt - 1) ->
-//     issue tile kt + 2 into tile kt - 1's buffer -> MFMAs on tile kt.
-template <int NB>
-constexpr int gemm_lds_per_tile() {
-	return (1 + NB) * BM / 8 / (THREADS / 64); // LDS-DMA instructions per thread per K tile
-}
 __device__ __forceinline__ void raw_barrier() {
 	asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-template <int N>
-__device__ __forceinline__ void vmcnt_wait() {
-	asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// WIDE: a 128 x 256 output tile for a single weight matrix, run as NB = 2 with
-// the two B tiles = columns [col0, col0 + 128) and [col0 + 128, col0 + 256) of
-// the same B: twice the MFMAs per A fragment read from LDS (the GLU kernel's
-// shape, ~1 PF/s where the 128 x 128 tile reached 0.55-0.75); the narrow
-// epilogue runs once per column half.
-template <class EPI, int NB, int NS, bool WIDE = false>
-__global__ __launch_bounds__(THREADS) void gemm_nt_kernel(const uint16_t *__restrict__ A, int M, int K, BSrc B0,
-                                                          BSrc B1, int N, EPI epi) {
-	extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-	constexpr int BUF = (1 + NB) * TILE; // f16 per buffer
-	const int lane = threadIdx.x & 63;
-	const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-	const int wm = wave >> 1, wn = wave & 1;
-	const int h = lane >> 5, l32 = lane & 31;
-
-	// tile index: XCD-aware (blocks b, b+8, ... share an XCD's L2): consecutive
-	// tiles of one XCD walk down M for a fixed N panel (the W panel is reused)
-	static_assert(!WIDE || NB == 2, "the wide tile runs as two B tiles");
-	constexpr int TBN = WIDE ? 2 * BN : BN; // output columns per tile
-	const int tiles_m = (M + BM - 1) / BM, tiles_n = N / TBN;
-	const int nwg = tiles_m * tiles_n;
-	int wg = blockIdx.x;
-	{
-		const int q = nwg / 8, rr = nwg % 8, xcd = wg % 8, idx = wg / 8;
-		wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
-	}
-	const int tm = wg % tiles_m, tn = wg / tiles_m;
-	const int row0 = tm * BM, col0 = tn * TBN;
-
-	f32x16_t acc[NB][2][2];
-#pragma unroll
-	for (int b = 0; b < NB; ++b)
-#pragma unroll
-		for (int i = 0; i < 2; ++i)
-#pragma unroll
-			for (int j = 0; j < 2; ++j)
-				acc[b][i][j] = f32x16_t{};
-
-	const int nk = K / BK;
-	const uint16_t *w0, *w1 = nullptr;
-	int w0r, w0n, w1r = 0, w1n = 1;
-	B0.tile(col0, w0, w0r, w0n);
-	if constexpr (NB == 2)
-		B1.tile(WIDE ? col0 + BN : col0, w1, w1r, w1n);
-	auto stage = [&](int buf, int kt) {
-		uint16_t *base = smem + buf * BUF;
-		stage_tile(base, A, K, row0, M, kt * BK, wave, lane);
-		stage_tile(base + TILE, w0, K, w0r, w0n, kt * BK, wave, lane);
-		if constexpr (NB == 2)
-			stage_tile(base + 2 * TILE, w1, K, w1r, w1n, kt * BK, wave, lane);
-	};
-	auto compute = [&](const uint16_t *a_t) {
-#pragma unroll
-		for (int s = 0; s < BK / 16; ++s) {
-			half8_t af[2], bf[NB][2];
-#pragma unroll
-			for (int i = 0; i < 2; ++i)
-				af[i] = frag(a_t, wm * 64 + 32 * i + l32, s, h);
-#pragma unroll
-			for (int b = 0; b < NB; ++b)
-#pragma unroll
-				for (int j = 0; j < 2; ++j)
-					bf[b][j] = frag(a_t + (1 + b) * TILE, wn * 64 + 32 * j + l32, s, h);
-#pragma unroll
-			for (int b = 0; b < NB; ++b)
-#pragma unroll
-				for (int i = 0; i < 2; ++i)
-#pragma unroll
-					for (int j = 0; j < 2; ++j)
-						acc[b][i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[b][j], acc[b][i][j], 0, 0, 0);
-		}
-	};
-	if constexpr (NS == 2) {
-		stage(0, 0);
-		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-		__syncthreads();
-		int cur = 0;
-		for (int kt = 0; kt < nk; ++kt) {
-			if (kt + 1 < nk)
-				stage(cur ^ 1, kt + 1);
-			compute(smem + cur * BUF);
-			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-			__syncthreads();
-			cur ^= 1;
-		}
-	} else {
-		constexpr int L = gemm_lds_per_tile<NB>();
-		stage(0, 0);
-		if (nk > 1)
-			stage(1, 1);
-		int cur = 0; // buffer of tile kt
-		for (int kt = 0; kt < nk; ++kt) {
-			if (kt + 1 < nk)
-				vmcnt_wait<L>(); // tile kt landed (this thread's DMAs); tile kt + 1 may stay in flight
-			else
-				vmcnt_wait<0>();
-			raw_barrier();
-			if (kt + 2 < nk)
-				stage(cur == 0 ? 2 : cur - 1, kt + 2); // tile kt - 1's buffer: every wave is past reading it
-			compute(smem + cur * BUF);
-			cur = cur == 2 ? 0 : cur + 1;
-		}
-		raw_barrier(); // the epilogue may reuse the staging buffers (EpiLogits)
-	}
-	EPI e = epi;
-	if constexpr (EPI::NEEDS_LDS)
-		e.red = (float *)smem; // the staging buffers are free after the K loop's last barrier
-	if constexpr (WIDE) {
-		typedef f32x16_t half_acc_t[1][2][2];
-		e.template apply<1>(*reinterpret_cast<half_acc_t *>(&acc[0]), row0 + wm * 64, col0 + wn * 64, lane);
-		if constexpr (EPI::NEEDS_LDS)
-			__syncthreads(); // the first half's readers are done with e.red
-		e.template apply<1>(*reinterpret_cast<half_acc_t *>(&acc[1]), row0 + wm * 64, col0 + BN + wn * 64, lane);
-	} else {
-		e.template apply<NB>(acc, row0 + wm * 64, col0 + wn * 64, lane);
-	}
 }
 
 // ---------------------------------------------------------------- attention
@@ -620,7 +292,11 @@ __global__ __launch_bounds__(256) void embed_rows_kernel(const int *__restrict__
 	}
 }
 
-// Xn[t] = f16(rmsnorm(X[t]) * w)  (rmsnorm, infer.cpp:134-144 statement order)
+// Xn[t] = f16(rmsnorm(X[t]) * w)  (rmsnorm, infer.cpp:134-144 statement order).
+// SPLIT: row t of Xn is [hi | lo], 2 dim wide: hi = f16(v), lo = f16(v - hi), so
+// hi + lo carries v to ~22 bits (the K / V columns of the QKV GEMM run over both
+// halves against the same weight row; prefill_gemm.h BWrap).
+template <bool SPLIT>
 __global__ __launch_bounds__(256) void rmsnorm_rows_kernel(const float *__restrict__ X, const float *__restrict__ w,
                                                            int dim, float eps, uint16_t *__restrict__ Xn) {
 	__shared__ float red[4];
@@ -637,14 +313,26 @@ __global__ __launch_bounds__(256) void rmsnorm_rows_kernel(const float *__restri
 	__syncthreads();
 	const float tot = red[0] + red[1] + red[2] + red[3];
 	const float scale = 1.0f / sqrtf(tot / dim + eps);
+	uint16_t *row = Xn + (size_t)t * dim * (SPLIT ? 2 : 1);
 	for (int i = threadIdx.x * 4; i < dim; i += 256 * 4) {
 		const float4_t v = *(const float4_t *)(x + i);
 		const float4_t g = *(const float4_t *)(w + i);
-		uint16_t *o = Xn + (size_t)t * dim + i;
-		o[0] = f2h_bits(v[0] * scale * g[0]);
-		o[1] = f2h_bits(v[1] * scale * g[1]);
-		o[2] = f2h_bits(v[2] * scale * g[2]);
-		o[3] = f2h_bits(v[3] * scale * g[3]);
+		float y[4];
+		uint16_t hb[4];
+#pragma unroll
+		for (int e = 0; e < 4; ++e) {
+			y[e] = v[e] * scale * g[e];
+			hb[e] = f2h_bits(y[e]);
+		}
+		*(uint2 *)(row + i) = make_uint2(hb[0] | ((uint32_t)hb[1] << 16), hb[2] | ((uint32_t)hb[3] << 16));
+		if constexpr (SPLIT) {
+			uint16_t lb[4];
+#pragma unroll
+			for (int e = 0; e < 4; ++e)
+				lb[e] = f2h_bits(y[e] - h2f(hb[e]));
+			*(uint2 *)(row + dim + i) =
+			    make_uint2(lb[0] | ((uint32_t)lb[1] << 16), lb[2] | ((uint32_t)lb[3] << 16));
+		}
 	}
 }
 

@@ -1,11 +1,16 @@
-// prefill_gemm.h — the prefill's large-tile MFMA GEMM: C = A · W^T with a
-// 256-row output tile per workgroup and 8 waves, for the shapes where the
-// 128 x 128 tile of prefill.h (gemm_nt_kernel) is bound by LDS traffic.
+// prefill_gemm.h — the prefill's MFMA GEMMs: C = A · W^T with a 256-row output
+// tile per workgroup and 8 waves (the round-2 128 x 128 tile, bound by LDS
+// traffic, was removed in round 4).
 //
-// Why a bigger tile: an MFMA needs its A and B fragments read from LDS. With
-// the 128 x 128 tile each of the 4 waves owns 64 x 64 outputs and reads one
+// A is [M][lda] f16 and the GEMM runs over K of its columns; B rows are K_b = kb
+// wide and column k >= kb of the product reads B column k - kb ("B wrap"): with
+// A = [hi | lo] (2 kb wide) that is C = hi W^T + lo W^T, the split-f16 A operand of
+// the QKV GEMM's K / V columns (prefill.h rmsnorm_rows_kernel<true>).
+//
+// Why a big tile: an MFMA needs its A and B fragments read from LDS. With
+// the 128 x 128 tile of round 2 each of the 4 waves owned 64 x 64 outputs and read one
 // 1-KB fragment per 32x32x16 MFMA (4 reads per 4 MFMAs); the LDS-DMA fill of
-// the next K tile adds 32 KB per 64-deep step. Here each of the 8 waves owns
+// the next K tile added 32 KB per 64-deep step. Here each of the 8 waves owns
 // 128 x 64 (BN 256) or 64 x 64 (BN 128) outputs of a 256 x BN tile and issues
 // v_mfma_f32_16x16x32_f16: 12 fragment reads per 32 MFMAs (BN 256), and the
 // per-flop LDS-DMA traffic halves (cdna_hip_programming.md §5: the 256² tile is
@@ -312,8 +317,8 @@ __device__ __forceinline__ half8_t g16frag(const uint16_t *lds, int r, int s, in
 
 // C tile [256][BN] of C = A · B^T, B rows through BMAP. 8 waves as WM x (8 / WM).
 template <class EPI, class BMAP, int BN, int WM>
-__global__ __launch_bounds__(G_THREADS, 1) void gemm16_kernel(const uint16_t *__restrict__ A, int M, int K, BMAP bm,
-                                                             int N, EPI epi) {
+__global__ __launch_bounds__(G_THREADS, 1) void gemm16_kernel(const uint16_t *__restrict__ A, int lda, int M, int K,
+                                                             int kb, BMAP bm, int N, EPI epi, int c0) {
 	constexpr int WN = 8 / WM;
 	constexpr int TM = G_BM / WM, TN = BN / WN; // per-wave output
 	constexpr int FI = TM / 16, FJ = TN / 16;
@@ -336,15 +341,15 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm16_kernel(const uint16_t *__
 	}
 	const int tm = wg % tiles_m, tn = wg / tiles_m;
 	const int row0 = tm * G_BM;
-	const int colB = tn * (BN / BMAP::COLS_PER_TILE_DIV); // first B column (plain) / hidden column (GLU)
+	const int colB = c0 + tn * (BN / BMAP::COLS_PER_TILE_DIV); // first B column (plain) / hidden column (GLU)
 
 	const uint16_t *ap[NIA], *bp[NIB];
 #pragma unroll
 	for (int i = 0; i < NIA; ++i)
-		ap[i] = A + (size_t)min(row0 + (wave * NIA + i) * 8 + (lane >> 3), M - 1) * K;
+		ap[i] = A + (size_t)min(row0 + (wave * NIA + i) * 8 + (lane >> 3), M - 1) * lda;
 #pragma unroll
 	for (int i = 0; i < NIB; ++i)
-		bp[i] = bm.row(colB, (wave * NIB + i) * 8 + (lane >> 3), K);
+		bp[i] = bm.row(colB, (wave * NIB + i) * 8 + (lane >> 3), kb);
 
 	f32x4_t acc[FI][FJ];
 #pragma unroll
@@ -356,8 +361,9 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm16_kernel(const uint16_t *__
 	const int nk = K / G_BK;
 	auto stage = [&](int buf, int kt) {
 		uint16_t *base = smem + buf * BUF;
-		g16stage<NIA>(base, ap, kt * G_BK, wave, lane);
-		g16stage<NIB>(base + TA, bp, kt * G_BK, wave, lane);
+		const int k0 = kt * G_BK;
+		g16stage<NIA>(base, ap, k0, wave, lane);
+		g16stage<NIB>(base + TA, bp, k0 < kb ? k0 : k0 - kb, wave, lane); // B wrap
 	};
 	stage(0, 0);
 	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -441,8 +447,8 @@ constexpr size_t gemm16_lds() {
 constexpr int P8_HT = 128 * G_BK; // f16 per A half-tile (128 rows)
 
 template <class EPI, class BMAP, int FJ0 = 2, int FJ1 = 2>
-__global__ __launch_bounds__(G_THREADS, 1) void gemm8p_kernel(const uint16_t *__restrict__ A, int M, int K, BMAP bm,
-                                                             int N, EPI epi, int c0) {
+__global__ __launch_bounds__(G_THREADS, 1) void gemm8p_kernel(const uint16_t *__restrict__ A, int lda, int M, int K,
+                                                             int kb, BMAP bm, int N, EPI epi, int c0) {
 	constexpr int FI = 8, FJ = FJ0 + FJ1, TM = 128, TN = 16 * FJ, BN = 4 * TN;
 	constexpr int HB0 = 64 * FJ0 * G_BK, HB1 = 64 * FJ1 * G_BK; // f16 per B half-tile
 	constexpr int OFF[4] = {0, P8_HT, 2 * P8_HT, 2 * P8_HT + HB0}; // Am0, Am1, Bn0, Bn1 in a buffer
@@ -481,24 +487,25 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm8p_kernel(const uint16_t *__
 			const int lr = (2 * wave + i) * 8 + (lane >> 3);
 			const int sw = 8 * ((lane & 7) ^ (lr & 7));
 			const int ra = lr < 64 ? lr : lr + 64; // Am0 tile row; Am1 = + 64
-			aoff[0][i] = (uint32_t)min(row0 + ra, M - 1) * K + sw;
-			aoff[1][i] = (uint32_t)min(row0 + ra + 64, M - 1) * K + sw;
+			aoff[0][i] = (uint32_t)min(row0 + ra, M - 1) * lda + sw;
+			aoff[1][i] = (uint32_t)min(row0 + ra + 64, M - 1) * lda + sw;
 		}
 	#pragma unroll
 		for (int i = 0; i < FJ0; ++i) {
 			const int lr = (FJ0 * wave + i) * 8 + (lane >> 3);
 			const int sw = 8 * ((lane & 7) ^ (lr & 7));
-			bp[0][i] = bm.row(colB, (lr / (16 * FJ0)) * TN + lr % (16 * FJ0), K) + sw;
+			bp[0][i] = bm.row(colB, (lr / (16 * FJ0)) * TN + lr % (16 * FJ0), kb) + sw;
 		}
 	#pragma unroll
 		for (int i = 0; i < FJ1; ++i) {
 			const int lr = (FJ1 * wave + i) * 8 + (lane >> 3);
 			const int sw = 8 * ((lane & 7) ^ (lr & 7));
-			bp[1][i] = bm.row(colB, (lr / (16 * FJ1)) * TN + 16 * FJ0 + lr % (16 * FJ1), K) + sw;
+			bp[1][i] = bm.row(colB, (lr / (16 * FJ1)) * TN + 16 * FJ0 + lr % (16 * FJ1), kb) + sw;
 		}
 		// half-tile h (0 Am0, 1 Am1, 2 Bn0, 3 Bn1) of K tile kt into buffer buf
 		auto stage = [&](int buf, int h, int kt) {
 			const int k0 = kt * G_BK;
+			const int kw = k0 < kb ? k0 : k0 - kb; // B wrap
 			uint16_t *base = smem + buf * BUFE + OFF[h];
 			if (h < 2) {
 	#pragma unroll
@@ -508,12 +515,12 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm8p_kernel(const uint16_t *__
 			} else if (h == 2) {
 	#pragma unroll
 				for (int i = 0; i < FJ0; ++i)
-					__builtin_amdgcn_global_load_lds((const void *)(bp[0][i] + k0),
+					__builtin_amdgcn_global_load_lds((const void *)(bp[0][i] + kw),
 					                                 (YALM_LDS void *)(base + (FJ0 * wave + i) * 8 * G_BK), 16, 0, 0);
 			} else {
 	#pragma unroll
 				for (int i = 0; i < FJ1; ++i)
-					__builtin_amdgcn_global_load_lds((const void *)(bp[1][i] + k0),
+					__builtin_amdgcn_global_load_lds((const void *)(bp[1][i] + kw),
 					                                 (YALM_LDS void *)(base + (FJ1 * wave + i) * 8 * G_BK), 16, 0, 0);
 			}
 		};

@@ -264,6 +264,13 @@ static bool attn_supported(int head_dim, int G) {
 	       G <= 8;
 }
 
+// head mode up to this many 64-key chunks (attention.h attn_decode_body; A/B build:
+// YALM_ATTN_HEADMAX, 0 = key mode always)
+static int attn_head_max() {
+	static const int h = ab_env("YALM_ATTN_HEADMAX") ? std::max(0, atoi(ab_env("YALM_ATTN_HEADMAX"))) : ATTN_HEAD_MAX;
+	return h;
+}
+
 template <int D>
 static void launch_attn_D(int G, const float *q, const uint16_t *kc, const uint16_t *vc, const StepState *step,
                           int n_heads, int n_kv, int max_seq_len, int nsplit, unsigned long long *part, int layer,
@@ -275,9 +282,10 @@ static void launch_attn_D(int G, const float *q, const uint16_t *kc, const uint1
 	const int nchunks = (max_seq_len + attn_chunk<D>() - 1) / attn_chunk<D>();
 	const int S = std::min(nchunks, splits);
 	const int grid = n_kv * S + n_heads; // attention workgroups, then one merger per query head
+	const int hmax = attn_head_max();
 #define YALM_ATTN(GT)                                                                                                  \
 	attn_decode_kernel<D, GT><<<grid, ATTN_THREADS, 0, st>>>(q, kc, vc, step, n_heads, n_kv, max_seq_len, nsplit, S, \
-	                                                         part, layer, n_layers, err, out, att)
+	                                                         hmax, part, layer, n_layers, err, out, att)
 	if (G <= 1)
 		YALM_ATTN(1);
 	else if (G <= 2)
@@ -372,10 +380,19 @@ static int attn_wo_init(yalm_decoder_s *d) {
 	// the epoch is >= 1 from the first forward / yalm_block on)
 	const size_t gran = (size_t)c.n_layers * c.n_heads * c.head_dim;
 	TRY(dalloc(d, (void **)&d->awo_gran, sizeof(unsigned long long) * gran));
-	// key-chunk splits per kv head, as the standalone attention launch
+	// key-chunk splits per kv head: as the standalone attention launch, but the whole grid
+	// (attention, one merger per query head, Wo) must fit the co-resident workgroup slots:
+	// a workgroup past them is dispatched only when an earlier one exits, and at short
+	// contexts every attention workgroup without keys still holds its slot for the
+	// kv_len load (S 32 at Mistral: 256 + 32 + 256 = 544 > 512 slots put the last 32 Wo
+	// slices ~2 us late, fused launch 8.9 -> 11.2 us at kv 17)
+	const int n_wo = (c.dim + AWO_RPW - 1) / AWO_RPW;
+	const int slots = occ * device_cu_count();
+	const int fit = (slots - c.n_heads - n_wo) / c.n_kv_heads;
 	const char *senv = ab_env("YALM_AWO_SPLITS");
-	d->awo_S = std::min(nchunks, senv ? std::max(1, std::min(ATTN_MAX_SPLITS, atoi(senv))) : ATTN_SPLITS);
-	d->awo_nb = c.n_kv_heads * d->awo_S + c.n_heads + (c.dim + AWO_RPW - 1) / AWO_RPW;
+	d->awo_S = std::max(1, std::min(nchunks, senv ? std::max(1, std::min(ATTN_MAX_SPLITS, atoi(senv)))
+	                                                : std::min(ATTN_SPLITS, fit)));
+	d->awo_nb = c.n_kv_heads * d->awo_S + c.n_heads + n_wo;
 	const char *denv = ab_env("YALM_ATTN_WO_DELAY");
 	// default 0.2 us (fp16) / 0.5 us (fp8): the attention workgroups' K/V loads reach HBM
 	// ahead of the Wo stream. fp16 (33.5 MB, slice lands ~5.4 us, after the heads):
@@ -452,6 +469,7 @@ static int launch_attn_wo(yalm_decoder_s *d, const yalm_block_weights &w, int la
 	p.max_seq_len = c.max_seq_len;
 	p.nsplit = attn_nsplit(c.max_seq_len);
 	p.S = d->awo_S;
+	p.head_max = attn_head_max();
 	p.q_dim = c.n_heads * c.head_dim;
 	p.dim = c.dim;
 	p.part = d->part;
@@ -812,6 +830,7 @@ static int create_decoder(const yalm_config *config, const yalm_model_weights *w
 	const int q_dim = c.n_heads * c.head_dim, kv_dim = c.n_kv_heads * c.head_dim;
 	const int nsplit = attn_nsplit(c.max_seq_len);
 	d->tokens_cap = 1 << 16;
+	d->pf_forms = pf_forms_from_env();
 	d->eager = getenv("YALM_EAGER") && atoi(getenv("YALM_EAGER")) != 0;
 	d->graph_sync = getenv("YALM_GRAPH_SYNC") && atoi(getenv("YALM_GRAPH_SYNC")) != 0;
 	// geometry overrides for A/B runs without a rebuild (same meaning as yalm_set_gemv_config):
