@@ -23,25 +23,33 @@ def main():
     ap.add_argument("--dtype", default="fp16", choices=["fp16", "fp8"])
     ap.add_argument("--iters", type=int, default=64)
     ap.add_argument("--ctx", type=int, default=16, help="positions hydrated first (attention kv_len = ctx + 1)")
+    ap.add_argument("--ctxs", default="", help="comma-separated contexts, hydrated progressively (overrides --ctx)")
+    ap.add_argument("--kernels", default="", help="comma-separated kernel ids (default: all)")
     args = ap.parse_args()
     runtime.check(runtime.lib.yalm_set_device(0))
     cfg = M.PRESETS[args.model].with_(weight_dtype=M.F16 if args.dtype == "fp16" else M.F8E5M2)
     dm = runtime.DeviceModel.synthetic(cfg, seed=1)
     dec = runtime.Decoder(dm)
-    for pos in range(args.ctx):
-        dec.forward((7 * pos + 1) % cfg.vocab_size, pos, runtime.HYDRATE_KV_CACHE)
+    ctxs = [int(c) for c in args.ctxs.split(",")] if args.ctxs else [args.ctx]
+    kids = [int(k) for k in args.kernels.split(",")] if args.kernels else list(KINDS)
     wb = M.DTYPE_BYTES[cfg.weight_dtype]
     nbytes = {0: (cfg.q_dim + 2 * cfg.kv_dim) * cfg.dim * wb, 2: cfg.dim * cfg.q_dim * wb,
               3: 2 * cfg.hidden_dim * cfg.dim * wb, 4: cfg.dim * cfg.hidden_dim * wb,
               5: cfg.vocab_size * cfg.dim * wb, 8: cfg.dim * cfg.q_dim * wb}
     env = {k: v for k, v in os.environ.items() if k.startswith("YALM_")}
-    print(f"[{args.model} {args.dtype} kv_len {args.ctx + 1}] {env}")
-    for kid, name in KINDS.items():
-        if kid == 8 and not dec.attn_wo:
-            continue
-        us = dec.time_kernel(kid, args.iters) * 1e3
-        gbs = nbytes.get(kid, 0) / (us * 1e-6) / 1e9 if kid in nbytes else 0
-        print(f"  {kid} {name:10s} {us:8.2f} us  {gbs:7.0f} GB/s  {dec.kernel_name(kid)}")
+    done = 0
+    for ctx in ctxs:
+        for pos in range(done, ctx):
+            dec.forward((7 * pos + 1) % cfg.vocab_size, pos, runtime.HYDRATE_KV_CACHE)
+        done = ctx
+        dec.forward((7 * ctx + 1) % cfg.vocab_size, ctx)  # the step state at kv_len ctx + 1
+        print(f"[{args.model} {args.dtype} kv_len {ctx + 1}] {env}")
+        for kid in kids:
+            if kid == 8 and not dec.attn_wo:
+                continue
+            us = dec.time_kernel(kid, args.iters) * 1e3
+            gbs = nbytes.get(kid, 0) / (us * 1e-6) / 1e9 if kid in nbytes else 0
+            print(f"  {kid} {KINDS[kid]:10s} {us:8.2f} us  {gbs:7.0f} GB/s  {dec.kernel_name(kid)}", flush=True)
     dec.close()
     dm.close()
 

@@ -553,7 +553,7 @@ __device__ __forceinline__ bool attn_core(int g, int hq0, int Gh, int c_first, i
 }
 
 // One attention workgroup (kv head g, split s0 of S): speculative loads, then one of
-//   * HEAD mode (kv_len <= head_max chunks; workgroups s0 < G): query head s0 of the
+//   * HEAD mode (kv_len <= head_max chunks, S >= G; workgroups s0 < G): query head s0 of the
 //     group over ALL the chunks, written directly -- no partial, no merger hop, and a
 //     quarter of the per-wave arithmetic of a 4-head chunk (Mistral: G = 4). The G
 //     workgroups of a kv head read the same K/V rows (the 2nd .. Gth from L2).
@@ -602,7 +602,7 @@ __device__ __forceinline__ bool attn_decode_body(int g, int s0, int S, int head_
 	load_kv((hcand ? 0 : s0) * CHUNK, kA, vA);
 	const int kv_len = step->kv_len;
 	const int ns = (kv_len + CHUNK - 1) / CHUNK;
-	if (ns <= head_max) {
+	if (ns <= head_max && G <= S) { // (a grid with fewer splits than query heads per group: key mode)
 		if (!hcand)
 			return false; // whole workgroup leaves before any barrier
 		return attn_core<D, 1, GT, GRAN>(g, s0, 1, 0, 1, ns, true, 0, qv, kA, vA, kv_len, kc, vc, n_heads, n_kv_heads,
@@ -643,7 +643,7 @@ __device__ __forceinline__ bool attn_merge_body(int g, int hq, int S, int head_m
 	const int kv_len = step->kv_len;
 	const int ns = (kv_len + CHUNK - 1) / CHUNK;
 	const int nact = min(ns, S);
-	if (ns <= head_max || nact <= 1 || hq >= G)
+	if ((ns <= head_max && G <= S) || nact <= 1 || hq >= G)
 		return false; // head mode, or one workgroup held every key: nothing to merge
 	const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
 	const int nsw = (nact - wave + ATTN_WAVES - 1) / ATTN_WAVES; // this wave's splits: wave + 4 j, j < nsw
