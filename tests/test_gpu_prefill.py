@@ -190,6 +190,38 @@ def test_prefill_matches_decode(name, n):
     dm.close()
 
 
+@pytest.mark.parametrize("cfg_name", ["gqa-d128", "d768", "gelu-d128"])
+@pytest.mark.parametrize("n", [1, 5, 16, 17, 33, 64])
+def test_prefill_short_prompt_paths(cfg_name, n, monkeypatch):
+    """Short prompts (T <= 64) run the split-K skinny GEMMs (prefill_skinny.h): their
+    log p and the KV cache they leave (next decode step's logits) against the decode
+    engine and against the 256-row-tile path of the same prompt (YALM_PF_SKINNY=0);
+    every M-tile count 1..4 and the row tails."""
+    cfg = CFGS[cfg_name]
+    R = rt()
+    dm = R.DeviceModel.synthetic(cfg, seed=8)
+    tokens = np.random.default_rng(100 + n).integers(0, cfg.vocab_size, size=n).astype(np.int32)
+    dec_s = R.Decoder(dm)
+    monkeypatch.setenv("YALM_PF_SKINNY", "0")
+    dec_l = R.Decoder(dm)
+    monkeypatch.delenv("YALM_PF_SKINNY")
+    dec_d = R.Decoder(dm)
+    try:
+        lp_s, lp_l = dec_s.prefill(tokens), dec_l.prefill(tokens)
+        np.testing.assert_allclose(lp_s, lp_l, atol=2e-3)  # the same f16 operands, another f32 sum order
+        if n > 1:
+            assert np.max(np.abs(lp_s[: n - 1] - _decode_logprobs(dec_d, tokens))) <= LP_ATOL
+        dec_d.forward(int(tokens[-1]), n - 1)
+        nxt = 7
+        lg_s, lg_d = dec_s.forward(nxt, n), dec_d.forward(nxt, n)
+        assert np.max(np.abs(lg_s - lg_d)) / np.max(np.abs(lg_d)) < 5e-3
+    finally:
+        dec_s.close()
+        dec_l.close()
+        dec_d.close()
+        dm.close()
+
+
 def test_bench_prefill_leg():
     """bench.py's config-4 leg (the `prefill` object of the default line) on a small
     model: the fields the driver reads, a finite MFMA rate, and its spot check of the

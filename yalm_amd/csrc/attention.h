@@ -391,8 +391,8 @@ __device__ __forceinline__ bool attn_core(int g, int hq0, int Gh, int c_first, i
 				for (int i = 0; i < NK; ++i)
 #pragma unroll
 					for (int h = 0; h < GT; ++h)
-						if (valid[i] && h < G)
-							st_sc1(att_dbg + (size_t)(g * G + h) * max_seq_len + t0 + tl0 + i * RSTEP, sv[i][h]);
+						if (valid[i] && h < Gh)
+							st_sc1(att_dbg + (size_t)(hb + h) * max_seq_len + t0 + tl0 + i * RSTEP, sv[i][h]);
 			}
 			stamp(4);
 #pragma unroll

@@ -75,6 +75,8 @@ struct PrefillBufs {
 	float *pmax = nullptr, *psum = nullptr; // [cap][vocab / 128] logits partials
 	float *tgt_logit = nullptr, *lp = nullptr; // [cap]
 	float *rope = nullptr;                     // [cap][head_dim / 2][2]
+	float *skp = nullptr;                      // split-K partials of the short-prompt GEMMs (prefill_skinny.h)
+	size_t skp_floats = 0;
 };
 
 // Prefill GEMM forms (prefill.hip): per GEMM kind the large-tile width (-1 = auto,
@@ -84,6 +86,7 @@ struct PrefillBufs {
 struct PfForms {
 	int g16[6] = {-1, -1, -1, -1, -1, -1}; // qkv, wo, glu, w2, cls, test
 	bool p8 = true, persist = true;
+	bool no_skinny = false; // T <= 64: split-K skinny GEMMs (prefill_skinny.h) unless set
 };
 PfForms pf_forms_from_env();
 

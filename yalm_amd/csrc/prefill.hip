@@ -14,13 +14,15 @@
 #include "decoder.h"
 #include "prefill.h"
 #include "prefill_gemm.h"
+#include "prefill_skinny.h"
 
 // Large-tile GEMM form per GEMM kind (prefill_gemm.h): the tile width BN of the
 // 256-row tile. Default: auto -- the BN dividing N that minimises rounds x (BN + 64),
 // rounds = ceil(tiles / CUs): a 256-CU chip should get whole rounds of large tiles
 // (Llama-3B Wo / W2 N 3072 -> 192). YALM_PF_G16 = "qkv:256,wo:128,..." forces widths
 // (the exact-form tests), YALM_PF_8P=0 the 2-phase kernel, YALM_PF_PERSIST=0 one
-// workgroup per tile. All three are read once, at decoder creation (PfForms); the
+// workgroup per tile, YALM_PF_SKINNY=0 the large tiles at T <= 64 too (prefill_skinny.h
+// otherwise). All of them are read once, at decoder creation (PfForms); the
 // kernel-level test hook yalm_gemm_f16 reads them per call.
 PfForms pf_forms_from_env() {
 	static const char *names[6] = {"qkv", "wo", "glu", "w2", "cls", "test"};
@@ -36,6 +38,8 @@ PfForms pf_forms_from_env() {
 		f.p8 = atoi(e) != 0;
 	if (const char *e = getenv("YALM_PF_PERSIST"))
 		f.persist = atoi(e) != 0;
+	if (const char *e = getenv("YALM_PF_SKINNY"))
+		f.no_skinny = atoi(e) == 0;
 	return f;
 }
 
@@ -142,6 +146,75 @@ int launch_plain(const PfForms &f, int bn, const uint16_t *A, int lda, int M, in
 	return YALM_ERR_UNSUPPORTED;
 }
 
+// ---- short prompts (T <= SK_MAX_T): split-K skinny GEMMs (prefill_skinny.h)
+constexpr int SK_MAX_T = 64;
+
+// K splits of a skinny GEMM (or of the q / k | v pair, which share one partial buffer):
+// every K chunk a multiple of the kernel's 256-column step and <= 64 KB of A rows in
+// LDS; the fewest splits that give >= 512 workgroups (the weight stream needs the whole
+// chip), else the most. kn: (N, K) of each GEMM sharing the splits.
+int sk_pick_ks(std::initializer_list<std::pair<int, int>> kn, int TP) {
+	int best = -1, kmax = 0, nblk = 0;
+	for (auto &p : kn) {
+		kmax = std::max(kmax, p.second);
+		nblk += p.first / pf::SK_ROWS;
+	}
+	for (int ks = 1; ks <= kmax / pf::SK_KSTEP; ++ks) {
+		bool ok = true;
+		for (auto &p : kn) {
+			const int K = p.second;
+			ok = ok && K % ks == 0 && (K / ks) % pf::SK_KSTEP == 0 && (size_t)TP * (K / ks) * 2 <= 65536;
+		}
+		if (!ok)
+			continue;
+		best = ks;
+		if (nblk * ks >= 512)
+			break;
+	}
+	return best;
+}
+
+template <int MT, class BMAP>
+int launch_skinny_mt(const uint16_t *A, int lda, int T, int K, int kb, const BMAP &bm, int N, int KS, int c0, int Np,
+                     float *part, hipStream_t st) {
+	auto kern = pf::skinny_gemm_kernel<MT, BMAP>;
+	static bool attr = false;
+	if (!attr) {
+		HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
+		attr = true;
+	}
+	const int KC = K / KS;
+	const size_t lds = (size_t)16 * MT * KC * sizeof(uint16_t);
+	hipLaunchKernelGGL(kern, dim3((N / pf::SK_ROWS) * KS), dim3(256), lds, st, A, lda, T, K, kb, bm, N, KC, c0, Np,
+	                   part);
+	HIPCHK(hipGetLastError());
+	return YALM_OK;
+}
+
+template <class BMAP>
+int launch_skinny(const uint16_t *A, int lda, int T, int K, int kb, const BMAP &bm, int N, int KS, int c0, int Np,
+                  float *part, hipStream_t st) {
+	switch ((T + 15) / 16) {
+	case 1:
+		return launch_skinny_mt<1>(A, lda, T, K, kb, bm, N, KS, c0, Np, part, st);
+	case 2:
+		return launch_skinny_mt<2>(A, lda, T, K, kb, bm, N, KS, c0, Np, part, st);
+	case 3:
+		return launch_skinny_mt<3>(A, lda, T, K, kb, bm, N, KS, c0, Np, part, st);
+	default:
+		return launch_skinny_mt<4>(A, lda, T, K, kb, bm, N, KS, c0, Np, part, st);
+	}
+}
+
+template <bool GLU, class EPI>
+int launch_skinny_reduce(const float *part, int KS, int T, int Np, const EPI &epi, hipStream_t st) {
+	const int TP = 16 * ((T + 15) / 16);
+	const int waves = (TP / 16) * (Np / 64);
+	pf::skinny_reduce_kernel<4, GLU, EPI><<<(waves + 3) / 4, 256, 0, st>>>(part, KS, TP, T, Np, epi);
+	HIPCHK(hipGetLastError());
+	return YALM_OK;
+}
+
 pf::BSrc one(const void *w, int rows) {
 	pf::BSrc b{};
 	b.p[0] = b.p[1] = b.p[2] = (const uint16_t *)w;
@@ -207,6 +280,17 @@ int ensure_bufs(yalm_decoder_s *d) {
 	TRY(pf_alloc(d, (void **)&b.tgt_logit, cap * 4));
 	TRY(pf_alloc(d, (void **)&b.lp, cap * 4));
 	TRY(pf_alloc(d, (void **)&b.rope, cap * c.head_dim * 4));
+	{ // short-prompt split-K partials: the largest [KS][64][Np] of the layer's GEMMs
+		const int kv_dim = c.n_kv_heads * c.head_dim, TP = SK_MAX_T;
+		const int np_qkv = (int)q_dim + 2 * kv_dim;
+		const size_t sz[4] = {
+		    (size_t)std::max(1, sk_pick_ks({{(int)q_dim, c.dim}, {2 * kv_dim, 2 * c.dim}}, TP)) * np_qkv,
+		    (size_t)std::max(1, sk_pick_ks({{c.dim, (int)q_dim}}, TP)) * c.dim,
+		    (size_t)std::max(1, sk_pick_ks({{2 * c.hidden_dim, c.dim}}, TP)) * 2 * c.hidden_dim,
+		    (size_t)std::max(1, sk_pick_ks({{c.dim, c.hidden_dim}}, TP)) * c.dim};
+		b.skp_floats = (size_t)TP * *std::max_element(sz, sz + 4);
+		TRY(pf_alloc(d, (void **)&b.skp, b.skp_floats * 4));
+	}
 	b.cap = (int)cap;
 	return YALM_OK;
 }
@@ -248,6 +332,13 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 	const int bn_kv = pick_bn(f, PG_QKV, T, 2 * kv_dim, false);
 	const int bn_wo = pick_bn(f, PG_WO, T, c.dim, false);
 	const int bn_w2 = pick_bn(f, PG_W2, T, c.dim, false);
+	// short prompts: split-K skinny GEMMs (the 256-row tiles would leave most CUs idle)
+	const int TP = 16 * ((T + 15) / 16);
+	const int ks_qkv = sk_pick_ks({{q_dim, c.dim}, {2 * kv_dim, 2 * c.dim}}, TP);
+	const int ks_wo = sk_pick_ks({{c.dim, q_dim}}, TP);
+	const int ks_glu = sk_pick_ks({{2 * c.hidden_dim, c.dim}}, TP);
+	const int ks_w2 = sk_pick_ks({{c.dim, c.hidden_dim}}, TP);
+	const bool small = T <= SK_MAX_T && !f.no_skinny && ks_qkv > 0 && ks_wo > 0 && ks_glu > 0 && ks_w2 > 0;
 	for (int l = 0; l < c.n_layers; ++l) {
 		const yalm_block_weights &w = d->b[l];
 		// normalised x as [hi | lo] (2 dim per row): hi is the q columns' A operand, hi + lo
@@ -273,10 +364,18 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 			e.head_dim = c.head_dim;
 			e.pos0 = pos0;
 			e.clip = c.qkv_clip;
-			// QKV + clip + RoPE as two launches: q (K = dim over hi) and k | v from column
+			// QKV + clip + RoPE as two GEMMs: q (K = dim over hi) and k | v from column
 			// q_dim (K = 2 dim over hi | lo, the B rows wrapping at dim)
-			TRY(launch_plain(f, bn_q, b.Xn, 2 * c.dim, T, c.dim, c.dim, qkv, q_dim, e, st));
-			TRY(launch_plain(f, bn_kv, b.Xn, 2 * c.dim, T, 2 * c.dim, c.dim, qkv, 2 * kv_dim, e, st, q_dim));
+			if (small) {
+				const pf::BRowsPlain bm{qkv};
+				const int np = q_dim + 2 * kv_dim;
+				TRY(launch_skinny(b.Xn, 2 * c.dim, T, c.dim, c.dim, bm, q_dim, ks_qkv, 0, np, b.skp, st));
+				TRY(launch_skinny(b.Xn, 2 * c.dim, T, 2 * c.dim, c.dim, bm, 2 * kv_dim, ks_qkv, q_dim, np, b.skp, st));
+				TRY(launch_skinny_reduce<false>(b.skp, ks_qkv, T, np, e, st));
+			} else {
+				TRY(launch_plain(f, bn_q, b.Xn, 2 * c.dim, T, c.dim, c.dim, qkv, q_dim, e, st));
+				TRY(launch_plain(f, bn_kv, b.Xn, 2 * c.dim, T, 2 * c.dim, c.dim, qkv, 2 * kv_dim, e, st, q_dim));
+			}
 		}
 		TRY(launch_attn_prefill(b.Q, w.key_cache, w.value_cache, T, pos0, c.n_heads, c.n_kv_heads, c.head_dim, b.O,
 		                        st));
@@ -285,18 +384,45 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 			e.x = b.X;
 			e.ldx = c.dim;
 			e.M = T;
-			TRY(launch_plain(f, bn_wo, b.O, q_dim, T, q_dim, q_dim, one(w.wo, c.dim), c.dim, e, st));
+			if (small) {
+				TRY(launch_skinny(b.O, q_dim, T, q_dim, q_dim, pf::BRowsPlain{one(w.wo, c.dim)}, c.dim, ks_wo, 0, c.dim,
+				                  b.skp, st));
+				TRY(launch_skinny_reduce<false>(b.skp, ks_wo, T, c.dim, e, st));
+			} else {
+				TRY(launch_plain(f, bn_wo, b.O, q_dim, T, q_dim, q_dim, one(w.wo, c.dim), c.dim, e, st));
+			}
 		}
 		pf::rmsnorm_rows_kernel<false><<<T, 256, 0, st>>>(b.X, w.rms_ffn, c.dim, c.norm_eps, b.Xn);
 		HIPCHK(hipGetLastError());
-		TRY(c.act == YALM_SILU ? enqueue_glu<1>(d, w, T) : enqueue_glu<0>(d, w, T));
+		if (small) {
+			const pf::BRowsGlu<64> bm{(const uint16_t *)w.w1, (const uint16_t *)w.w3};
+			TRY(launch_skinny(b.Xn, c.dim, T, c.dim, c.dim, bm, 2 * c.hidden_dim, ks_glu, 0, 2 * c.hidden_dim, b.skp,
+			                  st));
+			if (c.act == YALM_SILU) {
+				pf::E16Glu<1> e;
+				e.h = b.H, e.ldh = c.hidden_dim, e.M = T;
+				TRY(launch_skinny_reduce<true>(b.skp, ks_glu, T, 2 * c.hidden_dim, e, st));
+			} else {
+				pf::E16Glu<0> e;
+				e.h = b.H, e.ldh = c.hidden_dim, e.M = T;
+				TRY(launch_skinny_reduce<true>(b.skp, ks_glu, T, 2 * c.hidden_dim, e, st));
+			}
+		} else {
+			TRY(c.act == YALM_SILU ? enqueue_glu<1>(d, w, T) : enqueue_glu<0>(d, w, T));
+		}
 		{
 			pf::E16Residual e;
 			e.x = b.X;
 			e.ldx = c.dim;
 			e.M = T;
-			TRY(launch_plain(f, bn_w2, b.H, c.hidden_dim, T, c.hidden_dim, c.hidden_dim, one(w.w2, c.dim), c.dim, e,
-			                 st));
+			if (small) {
+				TRY(launch_skinny(b.H, c.hidden_dim, T, c.hidden_dim, c.hidden_dim, pf::BRowsPlain{one(w.w2, c.dim)},
+				                  c.dim, ks_w2, 0, c.dim, b.skp, st));
+				TRY(launch_skinny_reduce<false>(b.skp, ks_w2, T, c.dim, e, st));
+			} else {
+				TRY(launch_plain(f, bn_w2, b.H, c.hidden_dim, T, c.hidden_dim, c.hidden_dim, one(w.w2, c.dim), c.dim, e,
+				                 st));
+			}
 		}
 	}
 	if (!want_lp)

@@ -1,0 +1,123 @@
+// prefill_skinny.h — the prefill's GEMMs for a SHORT prompt (T <= 64 rows: the
+// CLI's prompt hydration, main.cpp:91-97 in the reference, runs T one-token
+// forwards there). At small T the 256-row tiles of prefill_gemm.h leave most CUs
+// idle (Llama-3B Wo / W2, N 3072: 12-16 tiles) and the GEMM is a weight stream, not
+// MFMA work: every weight byte is read once, for T <= 64 rows.
+//
+//   skinny_gemm_kernel: split-K. Workgroup = 4 waves x 16 weight rows (64 rows of
+//     B) x KC columns of K; the A rows of its K chunk (T padded to 16 MT) are staged
+//     once in LDS (XOR-swizzled 16-byte chunks), the weight rows stream straight
+//     into registers (lane (row r, group q) reads 16 B at k + 8 q: 16 rows x 64 B per
+//     wave-instruction, U of them in flight) and feed v_mfma_f32_16x16x32_f16 with the
+//     TOKENS as the A operand and the weight rows as B. Each wave leaves its f32
+//     [16 MT][16] partial in part[ks][row][col].
+//   skinny_reduce_kernel: per (16 rows x 16 FJ columns) wave block, the KS partials
+//     summed in ks order (deterministic) into the 16x16 MFMA C layout, then the same
+//     epilogue object as the large-tile GEMM (prefill_gemm.h E16*: RoPE + cache
+//     write, residual add, GLU).
+// Columns k >= kb of A wrap to B column k - kb (the split-f16 K / V operand).
+#pragma once
+
+#include "prefill_gemm.h"
+
+namespace pf {
+
+constexpr int SK_ROWS = 64;    // B rows per workgroup (16 per wave)
+constexpr int SK_U = 8;        // weight loads in flight per lane (8 x 32 k)
+constexpr int SK_KSTEP = 32 * SK_U;
+
+// lds: [16 MT][KC] f16, 16-byte chunk c of row r stored at chunk c ^ (r & 15)
+template <int MT>
+__device__ __forceinline__ half8_t sk_afrag(const uint16_t *lds, int KC, int row, int k) {
+	const int c = (k >> 3) ^ (row & 15);
+	return *(const half8_t *)(lds + (size_t)row * KC + 8 * c);
+}
+
+// C[:, c0 .. c0 + N) partials over K columns of A (row stride lda; B rows kb wide,
+// wrapping), K chunks of KC: part[ks][row][c] with row stride Np (c absolute).
+template <int MT, class BMAP>
+__global__ __launch_bounds__(256) void skinny_gemm_kernel(const uint16_t *__restrict__ A, int lda, int T, int K,
+                                                          int kb, BMAP bm, int N, int KC, int c0, int Np,
+                                                          float *__restrict__ part) {
+	extern __shared__ __attribute__((aligned(16))) uint16_t as[];
+	const int nblk = N / SK_ROWS;
+	const int nb = blockIdx.x % nblk, ks = blockIdx.x / nblk;
+	const int k0 = ks * KC;
+	const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+	constexpr int TP = 16 * MT;
+	// ---- A rows [0, TP) x columns [k0, k0 + KC) into LDS (rows past T are zeros)
+	const int cpr = KC / 8; // 16-byte chunks per row
+	for (int i = tid; i < TP * cpr; i += 256) {
+		const int r = i / cpr, c = i % cpr;
+		u32x4_t v = u32x4_t{0u, 0u, 0u, 0u};
+		if (r < T)
+			v = *(const u32x4_t *)(A + (size_t)r * lda + k0 + 8 * c);
+		*(u32x4_t *)(as + (size_t)r * KC + 8 * (c ^ (r & 15))) = v;
+	}
+	// ---- this wave's 16 weight rows (through the row policy: plain / QKV segments / GLU)
+	const int cb = c0 + nb * SK_ROWS;           // the workgroup's first B row index (output column)
+	const int col = cb + 16 * wave;              // the wave's
+	const int kw0 = k0 < kb ? k0 : k0 - kb;      // B wrap (a K chunk never straddles kb)
+	// row policy: tile base = first output column (plain) or first hidden column (GLU:
+	// 64 B rows = 32 W1 rows then the same 32 W3 rows, BRowsGlu<64>)
+	const uint16_t *wrow =
+	    bm.row(cb / BMAP::COLS_PER_TILE_DIV, 16 * wave + (lane & 15), kb) + kw0 + 8 * (lane >> 4);
+	__syncthreads();
+	f32x4_t acc[MT];
+#pragma unroll
+	for (int m = 0; m < MT; ++m)
+		acc[m] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+	for (int k = 0; k < KC; k += SK_KSTEP) {
+		half8_t b[SK_U];
+#pragma unroll
+		for (int u = 0; u < SK_U; ++u)
+			b[u] = __builtin_bit_cast(half8_t, load_nt16(wrow + k + 32 * u));
+#pragma unroll
+		for (int u = 0; u < SK_U; ++u) {
+#pragma unroll
+			for (int m = 0; m < MT; ++m) {
+				const half8_t a = sk_afrag<MT>(as, KC, 16 * m + (lane & 15), k + 32 * u + 8 * (lane >> 4));
+				acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b[u], acc[m], 0, 0, 0);
+			}
+		}
+	}
+	// ---- partial: element r of acc[m] is row 16 m + 4 (lane >> 4) + r, column col + (lane & 15)
+	float *pp = part + (size_t)ks * TP * Np;
+#pragma unroll
+	for (int m = 0; m < MT; ++m)
+#pragma unroll
+		for (int r = 0; r < 4; ++r)
+			pp[(size_t)(16 * m + crow16(r, lane)) * Np + col + (lane & 15)] = acc[m][r];
+}
+
+// One wave per (16 rows, 16 FJ columns) block of C: the KS partials summed
+// in ks order, then epi.apply<1, FJ>(acc, row0, n0, ...) exactly as the large-tile GEMM's
+// epilogue sees its fragments. n0: the block's first output column, or (GLU) its first
+// hidden column (BRowsGlu: 16 FJ B rows = 8 FJ W1 rows then the same 8 FJ W3 rows).
+template <int FJ, bool GLU, class EPI>
+__global__ __launch_bounds__(256) void skinny_reduce_kernel(const float *__restrict__ part, int KS, int TP, int T,
+                                                            int N, EPI epi) {
+	const int lane = threadIdx.x & 63;
+	const int gw = blockIdx.x * 4 + (threadIdx.x >> 6); // global wave = block (row tile, col block)
+	const int ncb = N / (16 * FJ);
+	const int rt = gw / ncb, cb = gw % ncb;
+	if (rt * 16 >= T)
+		return;
+	f32x4_t acc[1][FJ];
+#pragma unroll
+	for (int j = 0; j < FJ; ++j) {
+		acc[0][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+		for (int r = 0; r < 4; ++r) {
+			const size_t off = (size_t)(16 * rt + crow16(r, lane)) * N + cb * 16 * FJ + 16 * j + (lane & 15);
+			float s = 0.0f;
+			for (int ks = 0; ks < KS; ++ks)
+				s += part[(size_t)ks * TP * N + off];
+			acc[0][j][r] = s;
+		}
+	}
+	const int n0 = GLU ? cb * 8 * FJ : cb * 16 * FJ;
+	epi.template apply<1, FJ>(acc, 16 * rt, n0, lane, 0, 1);
+}
+
+} // namespace pf
