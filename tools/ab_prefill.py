@@ -1,6 +1,7 @@
 """Interleaved A/B of prefill settings in ONE process (cdna_hip_programming.md §5.4
-rule 24): the environment knobs are read per launch, so each round runs every
-variant back to back on the same weights and device.
+rule 24): the forms are fixed when a decoder is created, so each variant gets its own
+decoder (created under its environment) and each round runs every variant back to
+back on the same weights and device.
 
 usage: python tools/ab_prefill.py [--model llama-3.2-3b] [--n 4096] [--rounds 5]
                                   name=ENV=VAL[;ENV=VAL...] ...
@@ -36,22 +37,25 @@ attn = 4 * cfg.head_dim * cfg.n_heads * n * (n + 1) // 2
 flops = cfg.n_layers * (gemm + attn) + 2 * n * cfg.dim * cfg.vocab_size
 
 dm = runtime.DeviceModel.synthetic(cfg, seed=5)
-dec = runtime.Decoder(dm)
-base = {k: os.environ.get(k) for _, env in variants for k in env}
+decs = {}
+for name, env in variants:
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    decs[name] = runtime.Decoder(dm)
+    for k, v in old.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
 res = {name: [] for name, _ in variants}
 for r in range(args.rounds):
-    for name, env in variants:
-        for k, v in base.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-        os.environ.update(env)
-        res[name].append(dec.prefill_time(n, args.iters))
+    for name, _ in variants:
+        res[name].append(decs[name].prefill_time(n, args.iters))
     print(json.dumps({"round": r, **{k: round(v[-1], 3) for k, v in res.items()}}), flush=True)
 for name, ms in res.items():
     s = sorted(ms)
     print(json.dumps({"variant": name, "model": args.model, "n": n, "median_ms": round(s[len(s) // 2], 3),
                       "min_ms": round(s[0], 3), "tflops_at_median": round(flops / (s[len(s) // 2] * 1e-3) / 1e12, 1)}))
-dec.close()
+for d in decs.values():
+    d.close()
 dm.close()

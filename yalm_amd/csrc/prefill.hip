@@ -149,26 +149,31 @@ int launch_plain(const PfForms &f, int bn, const uint16_t *A, int lda, int M, in
 // ---- short prompts (T <= SK_MAX_T): split-K skinny GEMMs (prefill_skinny.h)
 constexpr int SK_MAX_T = 64;
 
-// K splits of a skinny GEMM (or of the q / k | v pair, which share one partial buffer):
-// every K chunk a multiple of the kernel's 256-column step and <= 64 KB of A rows in
-// LDS; the fewest splits that give >= 512 workgroups (the weight stream needs the whole
-// chip), else the most. kn: (N, K) of each GEMM sharing the splits.
-int sk_pick_ks(std::initializer_list<std::pair<int, int>> kn, int TP) {
-	int best = -1, kmax = 0, nblk = 0;
+// K splits of a skinny GEMM: every K chunk a multiple of the kernel's 256-column step
+// and <= 64 KB of A rows in LDS; the fewest splits that give >= 512 workgroups (the
+// weight stream needs the whole chip), else the most. kn: (N, K, mult) of each GEMM
+// sharing one partial buffer, split mult x KS ways (the k | v GEMM over [hi | lo], K =
+// 2 dim, takes 2 KS splits of the q GEMM's chunk size, so no chunk straddles the B
+// wrap at dim).
+struct SkGemm {
+	int N, K, mult;
+};
+int sk_pick_ks(std::initializer_list<SkGemm> kn, int TP) {
+	int best = -1, kmin = 1 << 30, wg1 = 0;
 	for (auto &p : kn) {
-		kmax = std::max(kmax, p.second);
-		nblk += p.first / pf::SK_ROWS;
+		kmin = std::min(kmin, p.K / p.mult);
+		wg1 += p.N / pf::SK_ROWS * p.mult;
 	}
-	for (int ks = 1; ks <= kmax / pf::SK_KSTEP; ++ks) {
+	for (int ks = 1; ks <= kmin / pf::SK_KSTEP; ++ks) {
 		bool ok = true;
 		for (auto &p : kn) {
-			const int K = p.second;
-			ok = ok && K % ks == 0 && (K / ks) % pf::SK_KSTEP == 0 && (size_t)TP * (K / ks) * 2 <= 65536;
+			const int s = ks * p.mult;
+			ok = ok && p.K % s == 0 && (p.K / s) % pf::SK_KSTEP == 0 && (size_t)TP * (p.K / s) * 2 <= 65536;
 		}
 		if (!ok)
 			continue;
 		best = ks;
-		if (nblk * ks >= 512)
+		if (wg1 * ks >= 512)
 			break;
 	}
 	return best;
@@ -206,11 +211,13 @@ int launch_skinny(const uint16_t *A, int lda, int T, int K, int kb, const BMAP &
 	}
 }
 
+// columns < c_split sum KS partials, the others KS2
 template <bool GLU, class EPI>
-int launch_skinny_reduce(const float *part, int KS, int T, int Np, const EPI &epi, hipStream_t st) {
+int launch_skinny_reduce(const float *part, int KS, int KS2, int c_split, int T, int Np, const EPI &epi,
+                         hipStream_t st) {
 	const int TP = 16 * ((T + 15) / 16);
 	const int waves = (TP / 16) * (Np / 64);
-	pf::skinny_reduce_kernel<4, GLU, EPI><<<(waves + 3) / 4, 256, 0, st>>>(part, KS, TP, T, Np, epi);
+	pf::skinny_reduce_kernel<4, GLU, EPI><<<(waves + 3) / 4, 256, 0, st>>>(part, KS, KS2, c_split, TP, T, Np, epi);
 	HIPCHK(hipGetLastError());
 	return YALM_OK;
 }
@@ -283,11 +290,12 @@ int ensure_bufs(yalm_decoder_s *d) {
 	{ // short-prompt split-K partials: the largest [KS][64][Np] of the layer's GEMMs
 		const int kv_dim = c.n_kv_heads * c.head_dim, TP = SK_MAX_T;
 		const int np_qkv = (int)q_dim + 2 * kv_dim;
+		// (QKV: 2 KS partial slots, the k | v GEMM's)
 		const size_t sz[4] = {
-		    (size_t)std::max(1, sk_pick_ks({{(int)q_dim, c.dim}, {2 * kv_dim, 2 * c.dim}}, TP)) * np_qkv,
-		    (size_t)std::max(1, sk_pick_ks({{c.dim, (int)q_dim}}, TP)) * c.dim,
-		    (size_t)std::max(1, sk_pick_ks({{2 * c.hidden_dim, c.dim}}, TP)) * 2 * c.hidden_dim,
-		    (size_t)std::max(1, sk_pick_ks({{c.dim, c.hidden_dim}}, TP)) * c.dim};
+		    (size_t)2 * std::max(1, sk_pick_ks({{(int)q_dim, c.dim, 1}, {2 * kv_dim, 2 * c.dim, 2}}, TP)) * np_qkv,
+		    (size_t)std::max(1, sk_pick_ks({{c.dim, (int)q_dim, 1}}, TP)) * c.dim,
+		    (size_t)std::max(1, sk_pick_ks({{2 * c.hidden_dim, c.dim, 1}}, TP)) * 2 * c.hidden_dim,
+		    (size_t)std::max(1, sk_pick_ks({{c.dim, c.hidden_dim, 1}}, TP)) * c.dim};
 		b.skp_floats = (size_t)TP * *std::max_element(sz, sz + 4);
 		TRY(pf_alloc(d, (void **)&b.skp, b.skp_floats * 4));
 	}
@@ -334,10 +342,10 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 	const int bn_w2 = pick_bn(f, PG_W2, T, c.dim, false);
 	// short prompts: split-K skinny GEMMs (the 256-row tiles would leave most CUs idle)
 	const int TP = 16 * ((T + 15) / 16);
-	const int ks_qkv = sk_pick_ks({{q_dim, c.dim}, {2 * kv_dim, 2 * c.dim}}, TP);
-	const int ks_wo = sk_pick_ks({{c.dim, q_dim}}, TP);
-	const int ks_glu = sk_pick_ks({{2 * c.hidden_dim, c.dim}}, TP);
-	const int ks_w2 = sk_pick_ks({{c.dim, c.hidden_dim}}, TP);
+	const int ks_qkv = sk_pick_ks({{q_dim, c.dim, 1}, {2 * kv_dim, 2 * c.dim, 2}}, TP);
+	const int ks_wo = sk_pick_ks({{c.dim, q_dim, 1}}, TP);
+	const int ks_glu = sk_pick_ks({{2 * c.hidden_dim, c.dim, 1}}, TP);
+	const int ks_w2 = sk_pick_ks({{c.dim, c.hidden_dim, 1}}, TP);
 	const bool small = T <= SK_MAX_T && !f.no_skinny && ks_qkv > 0 && ks_wo > 0 && ks_glu > 0 && ks_w2 > 0;
 	for (int l = 0; l < c.n_layers; ++l) {
 		const yalm_block_weights &w = d->b[l];
@@ -370,8 +378,9 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 				const pf::BRowsPlain bm{qkv};
 				const int np = q_dim + 2 * kv_dim;
 				TRY(launch_skinny(b.Xn, 2 * c.dim, T, c.dim, c.dim, bm, q_dim, ks_qkv, 0, np, b.skp, st));
-				TRY(launch_skinny(b.Xn, 2 * c.dim, T, 2 * c.dim, c.dim, bm, 2 * kv_dim, ks_qkv, q_dim, np, b.skp, st));
-				TRY(launch_skinny_reduce<false>(b.skp, ks_qkv, T, np, e, st));
+				TRY(launch_skinny(b.Xn, 2 * c.dim, T, 2 * c.dim, c.dim, bm, 2 * kv_dim, 2 * ks_qkv, q_dim, np, b.skp,
+				                  st));
+				TRY(launch_skinny_reduce<false>(b.skp, ks_qkv, 2 * ks_qkv, q_dim, T, np, e, st));
 			} else {
 				TRY(launch_plain(f, bn_q, b.Xn, 2 * c.dim, T, c.dim, c.dim, qkv, q_dim, e, st));
 				TRY(launch_plain(f, bn_kv, b.Xn, 2 * c.dim, T, 2 * c.dim, c.dim, qkv, 2 * kv_dim, e, st, q_dim));
@@ -387,7 +396,7 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 			if (small) {
 				TRY(launch_skinny(b.O, q_dim, T, q_dim, q_dim, pf::BRowsPlain{one(w.wo, c.dim)}, c.dim, ks_wo, 0, c.dim,
 				                  b.skp, st));
-				TRY(launch_skinny_reduce<false>(b.skp, ks_wo, T, c.dim, e, st));
+				TRY(launch_skinny_reduce<false>(b.skp, ks_wo, ks_wo, c.dim, T, c.dim, e, st));
 			} else {
 				TRY(launch_plain(f, bn_wo, b.O, q_dim, T, q_dim, q_dim, one(w.wo, c.dim), c.dim, e, st));
 			}
@@ -401,11 +410,11 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 			if (c.act == YALM_SILU) {
 				pf::E16Glu<1> e;
 				e.h = b.H, e.ldh = c.hidden_dim, e.M = T;
-				TRY(launch_skinny_reduce<true>(b.skp, ks_glu, T, 2 * c.hidden_dim, e, st));
+				TRY(launch_skinny_reduce<true>(b.skp, ks_glu, ks_glu, 2 * c.hidden_dim, T, 2 * c.hidden_dim, e, st));
 			} else {
 				pf::E16Glu<0> e;
 				e.h = b.H, e.ldh = c.hidden_dim, e.M = T;
-				TRY(launch_skinny_reduce<true>(b.skp, ks_glu, T, 2 * c.hidden_dim, e, st));
+				TRY(launch_skinny_reduce<true>(b.skp, ks_glu, ks_glu, 2 * c.hidden_dim, T, 2 * c.hidden_dim, e, st));
 			}
 		} else {
 			TRY(c.act == YALM_SILU ? enqueue_glu<1>(d, w, T) : enqueue_glu<0>(d, w, T));
@@ -418,7 +427,7 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 			if (small) {
 				TRY(launch_skinny(b.H, c.hidden_dim, T, c.hidden_dim, c.hidden_dim, pf::BRowsPlain{one(w.w2, c.dim)},
 				                  c.dim, ks_w2, 0, c.dim, b.skp, st));
-				TRY(launch_skinny_reduce<false>(b.skp, ks_w2, T, c.dim, e, st));
+				TRY(launch_skinny_reduce<false>(b.skp, ks_w2, ks_w2, c.dim, T, c.dim, e, st));
 			} else {
 				TRY(launch_plain(f, bn_w2, b.H, c.hidden_dim, T, c.hidden_dim, c.hidden_dim, one(w.w2, c.dim), c.dim, e,
 				                 st));

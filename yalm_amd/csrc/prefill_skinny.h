@@ -15,7 +15,8 @@
 //     summed in ks order (deterministic) into the 16x16 MFMA C layout, then the same
 //     epilogue object as the large-tile GEMM (prefill_gemm.h E16*: RoPE + cache
 //     write, residual add, GLU).
-// Columns k >= kb of A wrap to B column k - kb (the split-f16 K / V operand).
+// Columns k >= kb of A wrap to B column k - kb (the split-f16 K / V operand); a K chunk
+// never straddles kb (the host splits the k | v GEMM in 2 KS chunks of the q GEMM's size).
 #pragma once
 
 #include "prefill_gemm.h"
@@ -94,15 +95,18 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(const uint16_t *__rest
 // in ks order, then epi.apply<1, FJ>(acc, row0, n0, ...) exactly as the large-tile GEMM's
 // epilogue sees its fragments. n0: the block's first output column, or (GLU) its first
 // hidden column (BRowsGlu: 16 FJ B rows = 8 FJ W1 rows then the same 8 FJ W3 rows).
+// Columns < c_split sum KS partial slots, the others KS2 (the QKV buffer: the k | v
+// GEMM ran 2 KS K chunks).
 template <int FJ, bool GLU, class EPI>
-__global__ __launch_bounds__(256) void skinny_reduce_kernel(const float *__restrict__ part, int KS, int TP, int T,
-                                                            int N, EPI epi) {
+__global__ __launch_bounds__(256) void skinny_reduce_kernel(const float *__restrict__ part, int KS, int KS2,
+                                                            int c_split, int TP, int T, int N, EPI epi) {
 	const int lane = threadIdx.x & 63;
 	const int gw = blockIdx.x * 4 + (threadIdx.x >> 6); // global wave = block (row tile, col block)
 	const int ncb = N / (16 * FJ);
 	const int rt = gw / ncb, cb = gw % ncb;
 	if (rt * 16 >= T)
 		return;
+	const int nks = cb * 16 * FJ < c_split ? KS : KS2;
 	f32x4_t acc[1][FJ];
 #pragma unroll
 	for (int j = 0; j < FJ; ++j) {
@@ -111,7 +115,7 @@ __global__ __launch_bounds__(256) void skinny_reduce_kernel(const float *__restr
 		for (int r = 0; r < 4; ++r) {
 			const size_t off = (size_t)(16 * rt + crow16(r, lane)) * N + cb * 16 * FJ + 16 * j + (lane & 15);
 			float s = 0.0f;
-			for (int ks = 0; ks < KS; ++ks)
+			for (int ks = 0; ks < nks; ++ks)
 				s += part[(size_t)ks * TP * N + off];
 			acc[0][j][r] = s;
 		}
