@@ -1,5 +1,5 @@
 #!/bin/bash
-# Build libyalm_hip.so from the sources of git revision $1 into yalm_amd/ab/libyalm_hip_$1.so
+# Build libyalm_hip.so from the sources of git revision $1 ("wt": the working tree) into yalm_amd/ab/libyalm_hip_$1.so
 # (for A/B runs on one box: YALM_LIB=<that path> python tools/kernel_times.py ...).
 # $2 = "ab": compile with -DYALM_AB (the tuning / tracing environment knobs, decoder.h ab_env)
 # into yalm_amd/ab/libyalm_hip_$1_ab.so.
@@ -9,7 +9,11 @@ def=""; suf=""
 if [ "$2" = "ab" ]; then def="-DYALM_AB"; suf="_ab"; fi
 root=$(cd "$(dirname "$0")/.." && pwd)
 tmp=$(mktemp -d)
-git -C "$root" archive "$rev" yalm_amd/csrc include | tar -x -C "$tmp"
+if [ "$rev" = wt ]; then  # the working tree
+  mkdir -p "$tmp/yalm_amd" && cp -r "$root/yalm_amd/csrc" "$tmp/yalm_amd/" && cp -r "$root/include" "$tmp/"
+else
+  git -C "$root" archive "$rev" yalm_amd/csrc include | tar -x -C "$tmp"
+fi
 mkdir -p "$root/yalm_amd/ab"
 for f in yalm_hip prefill; do
   extra=""; [ $f = prefill ] && extra="-mllvm -amdgpu-mfma-vgpr-form"

@@ -16,17 +16,18 @@
 // small (64 keys) so the KV read spreads over many CUs, and all K, V and q
 // loads are issued speculatively before kv_len is known (rows past kv_len are
 // read but masked), overlapping the step-state load.
-//  * kv_len <= CHUNK: the workgroup normalises and writes the heads directly.
-//    Longer contexts publish (max, sum, unnormalised out) per chunk as 8-byte
+//  * Short contexts (<= ATTN_HEAD_MAX chunks, "head mode"): one workgroup per
+//    query head runs all the keys and writes the head directly.
+//  * Longer contexts ("key mode"): the keys are split over S key splits per kv
+//    head; each split publishes per head (max, sum, unnormalised out) as 8-byte
 //    {value, tag} granules (one sc1 store each: the data is its own ready flag,
-//    MI355X_MICROARCH.md §visibility R2); the MERGER -- the highest-index
-//    workgroup with work for kv head g, so every workgroup it waits for was
-//    dispatched before it -- gathers all chunks' granules, re-reading until
-//    every tag holds this launch's tag, and merges them in chunk order
-//    (deterministic). Round 2 used a drained write + agent-scope arrival ticket
-//    + last-arriver merge: three serialised round trips instead of one.
-//    Tags: epoch * n_layers + layer, unique per (forward, layer), so the one
-//    partial buffer serves every layer and is never reset.
+//    MI355X_MICROARCH.md §visibility R2), and one MERGER workgroup per query head,
+//    dispatched after every attention workgroup of the launch, gathers them,
+//    re-reading until every tag holds this launch's tag, and folds them in a
+//    fixed order (deterministic). Tags: epoch * n_layers + layer, unique per
+//    (forward, layer), so the one partial buffer serves every layer and is never
+//    reset. Round 2 used a drained write + agent-scope arrival ticket +
+//    last-arriver merge: three serialised round trips instead of one.
 #pragma once
 
 #include <float.h>
@@ -229,13 +230,14 @@ __device__ __forceinline__ bool attn_core(int g, int hq0, int Gh, int c_first, i
 		}
 	};
 	// trace (attn_wo.h, thread 0 only): s_memrealtime + shader clock (s_memtime) at
-	// checkpoint k, kept in registers and stored at the end -- a store issued mid-way
-	// would queue behind the co-resident Wo workgroup's weight loads and stall the wave
-	unsigned long long tsr[8] = {}, tsc[8] = {};
+	// checkpoint k, kept in LDS and stored at the end -- a store issued mid-way would
+	// queue behind the co-resident Wo workgroup's weight loads and stall the wave, and
+	// 16 64-bit stamps kept in registers cost the fused kernel its second workgroup per CU
+	__shared__ unsigned long long tss[16];
 	auto stamp = [&](int k) {
 		if (ts) {
-			tsr[k] = __builtin_amdgcn_s_memrealtime();
-			tsc[k] = __builtin_amdgcn_s_memtime();
+			tss[k] = __builtin_amdgcn_s_memrealtime();
+			tss[8 + k] = __builtin_amdgcn_s_memtime();
 		}
 	};
 	auto flush = [&]() {
@@ -243,7 +245,7 @@ __device__ __forceinline__ bool attn_core(int g, int hq0, int Gh, int c_first, i
 #pragma unroll
 			for (int k = 2; k < 8; ++k)
 				if (k != 3)
-					ts[k] = tsr[k], ts[8 + k] = tsc[k];
+					ts[k] = tss[k], ts[8 + k] = tss[8 + k];
 		}
 	};
 	if (trace_on) { // tracing only: when the first chunk's loads have landed in every wave
@@ -552,19 +554,26 @@ __device__ __forceinline__ bool attn_core(int g, int hq0, int Gh, int c_first, i
 	return final_out;
 }
 
-// One attention workgroup (kv head g, split s0 of S): speculative loads, then one of
-//   * HEAD mode (kv_len <= head_max chunks, S >= G; workgroups s0 < G): query head s0 of the
-//     group over ALL the chunks, written directly -- no partial, no merger hop, and a
-//     quarter of the per-wave arithmetic of a 4-head chunk (Mistral: G = 4). The G
-//     workgroups of a kv head read the same K/V rows (the 2nd .. Gth from L2).
-//   * KEY mode (longer contexts): every query head of the group over chunks s0,
-//     s0 + S, ...: one partial per head for the mergers (or, with one workgroup holding
-//     keys, the head outputs).
-// The speculative first-chunk rows are chunk 0 for s0 < G (head mode's) and chunk s0
-// otherwise; a key-mode workgroup 0 < s0 < G re-issues its own.
+// One attention workgroup: unit u of kv head g's S + G - 1 units. Units u < G are HEAD
+// units (query head u of the group), units u >= G are SPLIT units (every query head of
+// the group, key split s = u - G + 1). Speculative loads first (q, the unit's first
+// chunk, which is known before kv_len: chunk 0 for a head unit, chunk s for a split
+// unit), then one of
+//   * HEAD mode (kv_len <= head_max chunks): head unit u runs query head u over ALL
+//     the chunks and writes it directly -- no partial, no merger hop, and a quarter of
+//     the per-wave arithmetic of a 4-head chunk (Mistral: G = 4). The G head units of a
+//     kv head read the same K/V rows (dispatched to the same XCD: the 2nd .. Gth from L2).
+//   * KEY mode (longer contexts): key split 0 (chunks 0, S, 2S, ...) is run by the G head
+//     units, one query head each; split s >= 1 (chunks s, s + S, ...) by split unit
+//     s + G - 1 for every head; one partial per (head, split) for the mergers (or, with
+//     only split 0 holding keys, the head outputs).
+// Round 4's first cut made units s0 < G both the head-mode units and key-mode split s0:
+// they speculated on chunk 0, so key-mode units 1 .. G-1 re-issued their own chunk
+// after kv_len (a load latency: Mistral kv 501 attention 7.0 us), and loading both
+// guesses cost the short contexts 0.5 us.
 // Returns true on a workgroup that wrote head outputs.
 template <int D, int GT, bool GRAN>
-__device__ __forceinline__ bool attn_decode_body(int g, int s0, int S, int head_max, const float *q,
+__device__ __forceinline__ bool attn_decode_body(int g, int u, int S, int head_max, const float *q,
                                                  const uint16_t *kc, const uint16_t *vc, const StepState *step,
                                                  int n_heads, int n_kv_heads, int max_seq_len, int nsplit,
                                                  unsigned long long *part, unsigned ptag, float *out, float *att_dbg,
@@ -581,6 +590,8 @@ __device__ __forceinline__ bool attn_decode_body(int g, int s0, int S, int head_
 	const int lane = threadIdx.x & 63;
 	const int tl0 = (threadIdx.x >> 6) * KPW + lane / LPK;
 	const int piece = lane % LPK;
+	const bool hu = u < G;             // head unit (query head u)
+	const int s = hu ? 0 : u - G + 1; // key split
 	auto load_kv = [&](int t0, u32x4_t (&kw)[NK], u32x4_t (&vw)[NK]) {
 #pragma unroll
 		for (int i = 0; i < NK; ++i) {
@@ -591,30 +602,31 @@ __device__ __forceinline__ bool attn_decode_body(int g, int s0, int S, int head_
 		}
 	};
 	// ---- speculative loads: q of the group's G heads (G * D contiguous floats, QL
-	// 16-byte pieces per lane), a first chunk's K/V rows (clamped to the cache), step
+	// 16-byte pieces per lane), the unit's first chunk's K/V rows (clamped to the cache)
 	const int gq = G * D;
 	float4_t qv[QL];
 #pragma unroll
 	for (int j = 0; j < QL; ++j)
 		qv[j] = *(const float4_t *)(q + (size_t)g * gq + min((j * 64 + lane) * 4, gq - 4));
-	const bool hcand = s0 < G;
 	u32x4_t kA[NK], vA[NK];
-	load_kv((hcand ? 0 : s0) * CHUNK, kA, vA);
+	load_kv(s * CHUNK, kA, vA);
 	const int kv_len = step->kv_len;
 	const int ns = (kv_len + CHUNK - 1) / CHUNK;
-	if (ns <= head_max && G <= S) { // (a grid with fewer splits than query heads per group: key mode)
-		if (!hcand)
+	if (ns <= head_max) { // (the host passes head_max >= 1, and >= every ns when S = 1)
+		if (!hu)
 			return false; // whole workgroup leaves before any barrier
-		return attn_core<D, 1, GT, GRAN>(g, s0, 1, 0, 1, ns, true, 0, qv, kA, vA, kv_len, kc, vc, n_heads, n_kv_heads,
+		return attn_core<D, 1, GT, GRAN>(g, u, 1, 0, 1, ns, true, 0, qv, kA, vA, kv_len, kc, vc, n_heads, n_kv_heads,
 		                                 max_seq_len, nsplit, part, ptag, out, att_dbg, gtag, ts, trace_on);
 	}
-	if (s0 * CHUNK >= kv_len)
+	if (s * CHUNK >= kv_len)
 		return false;
-	if (hcand && s0 != 0)
-		load_kv(s0 * CHUNK, kA, vA);
-	const int nact = min(ns, S); // workgroups of kv head g with keys: one partial each
-	return attn_core<D, GT, GT, GRAN>(g, 0, G, s0, S, ns, nact == 1, s0, qv, kA, vA, kv_len, kc, vc, n_heads,
-	                                  n_kv_heads, max_seq_len, nsplit, part, ptag, out, att_dbg, gtag, ts, trace_on);
+	// key mode: ns >= 2 and S >= 2, so every head has at least two partials and the
+	// mergers write the heads
+	if (hu)
+		return attn_core<D, 1, GT, GRAN>(g, u, 1, 0, S, ns, false, 0, qv, kA, vA, kv_len, kc, vc, n_heads, n_kv_heads,
+		                                 max_seq_len, nsplit, part, ptag, out, att_dbg, gtag, ts, trace_on);
+	return attn_core<D, GT, GT, GRAN>(g, 0, G, s, S, ns, false, s, qv, kA, vA, kv_len, kc, vc, n_heads, n_kv_heads,
+	                                  max_seq_len, nsplit, part, ptag, out, att_dbg, gtag, ts, trace_on);
 }
 
 // MERGER workgroup of (kv head g, query head h = g * G + hq): in key mode with
@@ -643,8 +655,8 @@ __device__ __forceinline__ bool attn_merge_body(int g, int hq, int S, int head_m
 	const int kv_len = step->kv_len;
 	const int ns = (kv_len + CHUNK - 1) / CHUNK;
 	const int nact = min(ns, S);
-	if ((ns <= head_max && G <= S) || nact <= 1 || hq >= G)
-		return false; // head mode, or one workgroup held every key: nothing to merge
+	if (ns <= head_max || hq >= G)
+		return false; // head mode (attn_decode_body): nothing to merge
 	const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
 	const int nsw = (nact - wave + ATTN_WAVES - 1) / ATTN_WAVES; // this wave's splits: wave + 4 j, j < nsw
 	const int dl = lane < D ? lane : 0; // lanes past D (D < 64) re-read dim 0 and only follow along
@@ -733,15 +745,16 @@ __device__ __forceinline__ bool attn_merge_body(int g, int hq, int S, int head_m
 	return true;
 }
 
-// Grid: n_kv * S attention workgroups (b = g + n_kv * s: (g, s) is dispatched after
-// (g', s') for every s' < s), then n_kv * G merger workgroups (g, hq).
+// Grid: n_kv * (S + G - 1) attention workgroups (b = g + n_kv * u: unit u of kv head g;
+// with n_kv a multiple of 8 a kv head's units share an XCD), then n_kv * G merger
+// workgroups (g, hq), dispatched after every attention workgroup.
 template <int D, int GT>
 __global__ __launch_bounds__(ATTN_THREADS) void attn_decode_kernel(
     const float *__restrict__ q, const uint16_t *__restrict__ kc, const uint16_t *__restrict__ vc,
     const StepState *__restrict__ step, int n_heads, int n_kv_heads, int max_seq_len, int nsplit, int S,
     int head_max, unsigned long long *__restrict__ part, int layer, int n_layers, unsigned *__restrict__ err,
     float *__restrict__ out, float *__restrict__ att_dbg) {
-	const int b = blockIdx.x, units = n_kv_heads * S;
+	const int b = blockIdx.x, units = n_kv_heads * (S + n_heads / n_kv_heads - 1);
 	const unsigned ptag = attn_part_tag(step, layer, n_layers);
 	if (b < units)
 		attn_decode_body<D, GT, false>(b % n_kv_heads, b / n_kv_heads, S, head_max, q, kc, vc, step, n_heads,

@@ -5,7 +5,7 @@
 // carries only the (small) KV read, and the Wo GEMV that follows starts its
 // 33.5 MB stream (Mistral-7B fp16) from a cold pipe. Here one grid holds two
 // kinds of workgroups:
-//   * ATTENTION workgroups [0, n_kv * S): attn_decode_body (attention.h), then
+//   * ATTENTION workgroups [0, n_kv * (S + G - 1)): attn_decode_body (attention.h), then
 //     n_kv * G MERGER workgroups (attn_merge_body); the workgroup that finishes
 //     a head (the single attention workgroup holding keys, or the head's merger)
 //     writes each head-output element as an 8-byte
@@ -46,7 +46,7 @@
 #define AWO_TRACE_N 16               // s_memrealtime + s_memtime stamps per workgroup (yalm_attn_wo_trace)
 
 struct AttnWoArgs {
-	int n_heads, n_kv, max_seq_len, nsplit, S; // S = key-chunk splits per kv head: n_kv * S attention workgroups
+	int n_heads, n_kv, max_seq_len, nsplit, S; // S = key splits per kv head: n_kv * (S + G - 1) attention workgroups
 	int head_max;                              // head mode up to this many 64-key chunks (attention.h)
 	int q_dim, dim;
 	unsigned long long *part; // attention chunk partials (n_heads, nsplit, D + 2) as tagged granules
@@ -173,8 +173,9 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 	constexpr int LPT = AWO_RPW * XS;
 	static_assert(ATTN_THREADS == 256 && ATTN_WAVES == 4, "4-wave workgroups: one 4-row reduction per wave");
 	const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-	const int units = p.n_kv * p.S;                      // attention workgroups
-	const int munits = units + p.n_kv * (p.n_heads / p.n_kv); // + one merger per query head
+	const int G = p.n_heads / p.n_kv;
+	const int units = p.n_kv * (p.S + G - 1); // attention workgroups (head units + split units)
+	const int munits = units + p.n_heads;     // + one merger per query head
 	// include/yalm_hip.h yalm_attn_wo_trace: [0] start, [1] hand-off signalled / Wo slice landed, ...
 	// (kept in registers, stored when the workgroup is done: see attention.h `stamp`)
 	unsigned long long *tr = p.trace && tid == 0 ? p.trace + (size_t)b * AWO_TRACE_N : nullptr;
@@ -209,6 +210,9 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 	// bounds (unconditional loads); rows below row0 belong to workgroup j - 1
 	const int lrow0 = min(row0, p.dim - AWO_RPW);
 	const char *wbase = p.wo + (size_t)lrow0 * p.q_dim * WT::BYTES;
+	// the residual rows this workgroup adds to, loaded first (nothing else in the launch
+	// writes x): the read-modify-write at the end costs no load round trip
+	const float xres = p.x[lrow0 + (tid & (AWO_RPW - 1))];
 	if (p.delay > 0) {
 		const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 		while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)p.delay)
@@ -256,7 +260,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 	const int row = lrow0 + tid;
 	if (tid < AWO_RPW && row >= row0) {
 		const float s = (rowpart[tid][0] + rowpart[tid][1]) + (rowpart[tid][2] + rowpart[tid][3]);
-		p.x[row] += s;
+		p.x[row] = xres + s;
 	}
 	if (tr) {
 		tr[3] = __builtin_amdgcn_s_memrealtime(), tr[11] = __builtin_amdgcn_s_memtime();

@@ -136,7 +136,7 @@ struct yalm_decoder_s {
 	// launch path: attention + Wo as one launch (attn_wo.h) when supported;
 	// YALM_ATTN_WO=0 selects the two separate kernels
 	bool attn_wo = false;
-	int awo_nb = 0;                  // grid: n_kv * awo_S attention + ceil(dim / AWO_RPW) Wo workgroups
+	int awo_nb = 0;                  // grid: n_kv * (awo_S + G - 1) attention + n_heads mergers + ceil(dim / AWO_RPW) Wo
 	int awo_S = 0;                   // key-chunk splits per kv head
 	unsigned long long *awo_trace = nullptr; // A/B build, YALM_ATTN_WO_TRACE=1: [grid][16] stamps of the last launch
 	int awo_delay = 0;               // ticks the Wo workgroups wait before their slice loads

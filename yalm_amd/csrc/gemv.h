@@ -15,6 +15,8 @@
 // Accumulation is fp32 (weights widened exactly: f16 -> f32, E5M2 -> f16 -> f32).
 #pragma once
 
+#include <type_traits>
+
 #include "device_common.h"
 
 #define GEMV_THREADS 256
@@ -65,7 +67,22 @@ struct PResidual {
 		for (int r = 0; r < R; ++r)
 			out[g * R + r] += acc[r];
 	}
+	// the residual rows, read before the weight stream (gemv_rb_kernel): the epilogue's
+	// read-modify-write then costs no load round trip at the tail
+	static constexpr bool PRE = true;
+	__device__ __forceinline__ float pre(int g, int r) const { return out[g * R + r]; }
+	__device__ __forceinline__ void finish_pre(int g, const float *acc, const float *xr) const {
+#pragma unroll
+		for (int r = 0; r < R; ++r)
+			out[g * R + r] = xr[r] + acc[r];
+	}
 };
+
+// policies with a pre(g, r) / finish_pre epilogue (PRE = true)
+template <class P, class = void>
+struct gemv_pre : std::false_type {};
+template <class P>
+struct gemv_pre<P, std::void_t<decltype(P::PRE)>> : std::bool_constant<P::PRE> {};
 
 // out[row] = base[row] + acc: the tensor-parallel Wo / W2 partial of rank 0,
 // which also carries the residual into the all-reduce (other ranks: PStore).
@@ -498,6 +515,13 @@ __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__re
 	XPre<NORM, THREADS> xp;
 	if (xregs)
 		prefetch_x<NORM, THREADS>(xp, x, normw, n); // ahead of the weight stream in vmcnt order
+	float xr[R] = {}; // PRE policies: the epilogue's rows of group threadIdx.x (clamped, unconditional)
+	if constexpr (gemv_pre<P>::value) {
+		const int g0 = min(b + min((int)threadIdx.x, max(ngl - 1, 0)) * NB, p.n_groups - 1);
+#pragma unroll
+		for (int r = 0; r < R; ++r)
+			xr[r] = p.pre(g0, r);
+	}
 	u32x4_t buf[U];
 #pragma unroll
 	for (int u = 0; u < U; ++u) {
@@ -550,7 +574,14 @@ __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__re
 				t += part[(gl * R + r) * W + w];
 			a[r] = t;
 		}
-		p.finish_all(b + gl * NB, a);
+		if constexpr (gemv_pre<P>::value) {
+			if (gl == (int)threadIdx.x)
+				p.finish_pre(b + gl * NB, a, xr);
+			else
+				p.finish_all(b + gl * NB, a);
+		} else {
+			p.finish_all(b + gl * NB, a);
+		}
 	}
 #ifdef YALM_WG_TRACE // tools/wg_timeline.hip: per-workgroup start/end (s_memrealtime, 100 MHz)
 	if (threadIdx.x == 0) {

@@ -46,6 +46,25 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(const uint16_t *__rest
 	const int k0 = ks * KC;
 	const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 	constexpr int TP = 16 * MT;
+	// ---- this wave's 16 weight rows (through the row policy: plain / QKV segments / GLU)
+	const int cb = c0 + nb * SK_ROWS;           // the workgroup's first B row index (output column)
+	const int col = cb + 16 * wave;              // the wave's
+	const int kw0 = k0 < kb ? k0 : k0 - kb;      // B wrap (a K chunk never straddles kb)
+	// row policy: tile base = first output column (plain) or first hidden column (GLU:
+	// 64 B rows = 32 W1 rows then the same 32 W3 rows, BRowsGlu<64>)
+	const uint16_t *wrow =
+	    bm.row(cb / BMAP::COLS_PER_TILE_DIV, 16 * wave + (lane & 15), kb) + kw0 + 8 * (lane >> 4);
+	// ---- the weight stream: a ring of SK_U 16-byte loads per lane (32 K columns each),
+	// the first SK_U issued before the A chunk is staged; every consumed slot is refilled
+	// SK_U steps ahead, unconditionally (past the chunk it re-reads step 0, an L2 hit:
+	// a conditional refill makes hipcc drain vmcnt to 0 before every load). Round 4's
+	// first cut loaded SK_U steps, waited, computed, loaded the next SK_U: one full
+	// memory latency per 256 K columns (Mistral T = 1 prefill: 3.8 TB/s).
+	const int nst = KC / 32;
+	half8_t b[SK_U];
+#pragma unroll
+	for (int u = 0; u < SK_U; ++u)
+		b[u] = __builtin_bit_cast(half8_t, load_nt16(wrow + 32 * (u < nst ? u : 0)));
 	// ---- A rows [0, TP) x columns [k0, k0 + KC) into LDS (rows past T are zeros)
 	const int cpr = KC / 8; // 16-byte chunks per row
 	for (int i = tid; i < TP * cpr; i += 256) {
@@ -55,31 +74,23 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(const uint16_t *__rest
 			v = *(const u32x4_t *)(A + (size_t)r * lda + k0 + 8 * c);
 		*(u32x4_t *)(as + (size_t)r * KC + 8 * (c ^ (r & 15))) = v;
 	}
-	// ---- this wave's 16 weight rows (through the row policy: plain / QKV segments / GLU)
-	const int cb = c0 + nb * SK_ROWS;           // the workgroup's first B row index (output column)
-	const int col = cb + 16 * wave;              // the wave's
-	const int kw0 = k0 < kb ? k0 : k0 - kb;      // B wrap (a K chunk never straddles kb)
-	// row policy: tile base = first output column (plain) or first hidden column (GLU:
-	// 64 B rows = 32 W1 rows then the same 32 W3 rows, BRowsGlu<64>)
-	const uint16_t *wrow =
-	    bm.row(cb / BMAP::COLS_PER_TILE_DIV, 16 * wave + (lane & 15), kb) + kw0 + 8 * (lane >> 4);
 	__syncthreads();
 	f32x4_t acc[MT];
 #pragma unroll
 	for (int m = 0; m < MT; ++m)
 		acc[m] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-	for (int k = 0; k < KC; k += SK_KSTEP) {
-		half8_t b[SK_U];
-#pragma unroll
-		for (int u = 0; u < SK_U; ++u)
-			b[u] = __builtin_bit_cast(half8_t, load_nt16(wrow + k + 32 * u));
+	for (int j0 = 0; j0 < nst; j0 += SK_U) {
 #pragma unroll
 		for (int u = 0; u < SK_U; ++u) {
+			const int j = j0 + u;
+			if (j < nst) {
 #pragma unroll
-			for (int m = 0; m < MT; ++m) {
-				const half8_t a = sk_afrag<MT>(as, KC, 16 * m + (lane & 15), k + 32 * u + 8 * (lane >> 4));
-				acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b[u], acc[m], 0, 0, 0);
+				for (int m = 0; m < MT; ++m) {
+					const half8_t a = sk_afrag<MT>(as, KC, 16 * m + (lane & 15), 32 * j + 8 * (lane >> 4));
+					acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b[u], acc[m], 0, 0, 0);
+				}
 			}
+			b[u] = __builtin_bit_cast(half8_t, load_nt16(wrow + 32 * (j + SK_U < nst ? j + SK_U : 0)));
 		}
 	}
 	// ---- partial: element r of acc[m] is row 16 m + 4 (lane >> 4) + r, column col + (lane & 15)
@@ -107,18 +118,43 @@ __global__ __launch_bounds__(256) void skinny_reduce_kernel(const float *__restr
 	if (rt * 16 >= T)
 		return;
 	const int nks = cb * 16 * FJ < c_split ? KS : KS2;
+	// the KS partials of this lane's 4 FJ values: all 4 FJ loads of 4 consecutive ks in
+	// flight at once, summed in ks order (deterministic; round 4's first cut ran one serial
+	// chain of KS dependent loads per value: 27 us per Wo / W2 reduce at T = 1)
 	f32x4_t acc[1][FJ];
+	size_t off[FJ][4];
 #pragma unroll
 	for (int j = 0; j < FJ; ++j) {
 		acc[0][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-		for (int r = 0; r < 4; ++r) {
-			const size_t off = (size_t)(16 * rt + crow16(r, lane)) * N + cb * 16 * FJ + 16 * j + (lane & 15);
-			float s = 0.0f;
-			for (int ks = 0; ks < nks; ++ks)
-				s += part[(size_t)ks * TP * N + off];
-			acc[0][j][r] = s;
-		}
+		for (int r = 0; r < 4; ++r)
+			off[j][r] = (size_t)(16 * rt + crow16(r, lane)) * N + cb * 16 * FJ + 16 * j + (lane & 15);
+	}
+	const size_t kstride = (size_t)TP * N;
+	int ks = 0;
+	for (; ks + 4 <= nks; ks += 4) {
+		float v[4][FJ][4];
+#pragma unroll
+		for (int q = 0; q < 4; ++q)
+#pragma unroll
+			for (int j = 0; j < FJ; ++j)
+#pragma unroll
+				for (int r = 0; r < 4; ++r)
+					v[q][j][r] = part[(size_t)(ks + q) * kstride + off[j][r]];
+#pragma unroll
+		for (int q = 0; q < 4; ++q)
+#pragma unroll
+			for (int j = 0; j < FJ; ++j)
+#pragma unroll
+				for (int r = 0; r < 4; ++r)
+					acc[0][j][r] += v[q][j][r];
+	}
+	for (; ks < nks; ++ks) {
+#pragma unroll
+		for (int j = 0; j < FJ; ++j)
+#pragma unroll
+			for (int r = 0; r < 4; ++r)
+				acc[0][j][r] += part[(size_t)ks * kstride + off[j][r]];
 	}
 	const int n0 = GLU ? cb * 8 * FJ : cb * 16 * FJ;
 	epi.template apply<1, FJ>(acc, 16 * rt, n0, lane, 0, 1);

@@ -265,10 +265,12 @@ static bool attn_supported(int head_dim, int G) {
 }
 
 // head mode up to this many 64-key chunks (attention.h attn_decode_body; A/B build:
-// YALM_ATTN_HEADMAX, 0 = key mode always)
-static int attn_head_max() {
-	static const int h = ab_env("YALM_ATTN_HEADMAX") ? std::max(0, atoi(ab_env("YALM_ATTN_HEADMAX"))) : ATTN_HEAD_MAX;
-	return h;
+// YALM_ATTN_HEADMAX). At least 1 (one chunk is key split 0 alone: the same work with a
+// merger hop more), and every context with one key split (S = 1): key mode needs two.
+// (A kernel-side `ns == 1 ||` cost the attention 44 VGPRs: 192 -> 236.)
+static int attn_head_max(int S, int nchunks) {
+	static const int h = ab_env("YALM_ATTN_HEADMAX") ? atoi(ab_env("YALM_ATTN_HEADMAX")) : ATTN_HEAD_MAX;
+	return S <= 1 ? nchunks : std::max(1, h);
 }
 
 template <int D>
@@ -281,8 +283,8 @@ static void launch_attn_D(int G, const float *q, const uint16_t *kc, const uint1
 	static const int splits = ab_env("YALM_ATTN_SPLITS") ? std::max(1, std::min(ATTN_MAX_SPLITS, atoi(ab_env("YALM_ATTN_SPLITS")))) : ATTN_SPLITS;
 	const int nchunks = (max_seq_len + attn_chunk<D>() - 1) / attn_chunk<D>();
 	const int S = std::min(nchunks, splits);
-	const int grid = n_kv * S + n_heads; // attention workgroups, then one merger per query head
-	const int hmax = attn_head_max();
+	const int grid = n_kv * (S + G - 1) + n_heads; // head + split units, then one merger per query head
+	const int hmax = attn_head_max(S, nchunks);
 #define YALM_ATTN(GT)                                                                                                  \
 	attn_decode_kernel<D, GT><<<grid, ATTN_THREADS, 0, st>>>(q, kc, vc, step, n_heads, n_kv, max_seq_len, nsplit, S, \
 	                                                         hmax, part, layer, n_layers, err, out, att)
@@ -388,11 +390,11 @@ static int attn_wo_init(yalm_decoder_s *d) {
 	// slices ~2 us late, fused launch 8.9 -> 11.2 us at kv 17)
 	const int n_wo = (c.dim + AWO_RPW - 1) / AWO_RPW;
 	const int slots = occ * device_cu_count();
-	const int fit = (slots - c.n_heads - n_wo) / c.n_kv_heads;
+	const int fit = (slots - c.n_heads - n_wo) / c.n_kv_heads - (G - 1); // key splits: S + G - 1 units per kv head
 	const char *senv = ab_env("YALM_AWO_SPLITS");
 	d->awo_S = std::max(1, std::min(nchunks, senv ? std::max(1, std::min(ATTN_MAX_SPLITS, atoi(senv)))
 	                                                : std::min(ATTN_SPLITS, fit)));
-	d->awo_nb = c.n_kv_heads * d->awo_S + c.n_heads + n_wo;
+	d->awo_nb = c.n_kv_heads * (d->awo_S + G - 1) + c.n_heads + n_wo;
 	const char *denv = ab_env("YALM_ATTN_WO_DELAY");
 	// default 0.2 us (fp16) / 0.5 us (fp8): the attention workgroups' K/V loads reach HBM
 	// ahead of the Wo stream. fp16 (33.5 MB, slice lands ~5.4 us, after the heads):
@@ -469,7 +471,7 @@ static int launch_attn_wo(yalm_decoder_s *d, const yalm_block_weights &w, int la
 	p.max_seq_len = c.max_seq_len;
 	p.nsplit = attn_nsplit(c.max_seq_len);
 	p.S = d->awo_S;
-	p.head_max = attn_head_max();
+	p.head_max = attn_head_max(d->awo_S, (c.max_seq_len + attn_chunk<128>() - 1) / attn_chunk<128>());
 	p.q_dim = c.n_heads * c.head_dim;
 	p.dim = c.dim;
 	p.part = d->part;
@@ -1211,7 +1213,7 @@ extern "C" int yalm_attn_wo_trace(yalm_decoder d, unsigned long long *host, size
 	if (workgroups)
 		*workgroups = d->awo_nb;
 	if (attention_workgroups)
-		*attention_workgroups = d->c.n_kv_heads * d->awo_S + d->c.n_heads;
+		*attention_workgroups = d->c.n_kv_heads * (d->awo_S + d->c.n_heads / d->c.n_kv_heads - 1) + d->c.n_heads;
 	return YALM_OK;
 }
 
