@@ -46,7 +46,7 @@ def test_gemm_exact_integers(M_, N, K):
 # one workgroup per tile instead of the persistent tile loop. The round-2 128 x 128
 # kernel and its stage / wide forms were removed in round 4.
 G16_ALL = "qkv:{0},wo:{0},glu:{0},w2:{0},cls:{0},test:{0}"
-FORMS = {"auto": {},
+FORMS = {"auto": {}, "auto-qkv2": {"YALM_PF_QKV1": "0"},
          "g16-256": {"YALM_PF_G16": G16_ALL.format(256)},
          "g16-256-2ph": {"YALM_PF_G16": G16_ALL.format(256), "YALM_PF_8P": "0"}, "g16-128": {"YALM_PF_G16": G16_ALL.format(128)},
          "g16-192": {"YALM_PF_G16": G16_ALL.format(192)},
@@ -138,11 +138,12 @@ CFGS = {
 
 
 @pytest.mark.parametrize("cfg_name", ["gqa-d128", "d768"])
-@pytest.mark.parametrize("form", ["auto", "g16-256", "g16-256-2ph", "g16-128", "g16-128-2ph", "g16-192",
+@pytest.mark.parametrize("form", ["auto", "auto-qkv2", "g16-256", "g16-256-2ph", "g16-128", "g16-128-2ph", "g16-192",
                                   "g16-192-2ph", "g16-320", "g16-256-nopersist"])
 def test_prefill_forms_match_decode(form, cfg_name, monkeypatch):
-    """The whole prefill in each GEMM form (incl. the vocab-tiled logits epilogue and
-    the k | v launch at a column offset over the [hi | lo] operand)."""
+    """The whole prefill in each GEMM form (incl. the vocab-tiled logits epilogue, the
+    one-launch two-depth QKV GEMM ("auto") and the k | v launch at a column offset over
+    the [hi | lo] operand ("auto-qkv2", forced widths))."""
     for k, v in FORMS[form].items():
         monkeypatch.setenv(k, v)
     cfg = CFGS[cfg_name]

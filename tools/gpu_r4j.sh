@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 o=gpurun_out/r4j
 mkdir -p $o
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
-  tests/test_gpu_kernels.py tests/test_gpu_attn_wo.py tests/test_gpu_decode.py tests/test_gpu_ref_infer.py tests/test_gpu_prefill.py > $o/tests.log 2>&1 || { echo "tests failed"; grep -E "FAILED|Error|error" $o/tests.log | head -20; tail -30 $o/tests.log; exit 1; }
+  tests/test_gpu_kernels.py tests/test_gpu_attn_wo.py tests/test_gpu_decode.py tests/test_gpu_ref_infer.py tests/test_gpu_prefill.py tests/test_gpu_prefill_llama.py > $o/tests.log 2>&1 || { echo "tests failed"; grep -E "FAILED|Error|error" $o/tests.log | head -20; tail -30 $o/tests.log; exit 1; }
 tail -2 $o/tests.log
 OLD=yalm_amd/ab/libyalm_hip_dc1e452_ab.so
 NEW=yalm_amd/ab/libyalm_hip_wt_ab.so
@@ -38,6 +38,9 @@ for dt in fp8 fp16; do
         python3 -c "import sys,json; d=json.loads(sys.stdin.readline()); print(d['value'])")
     echo "$dt $(basename $lib) bench(20): $v tok/s"
   done
+done
+for v in 1 0 1 0; do
+  echo "prefill QKV1=$v: $(YALM_PF_QKV1=$v timeout -k 10 300 python tools/bench_prefill.py --iters 3 --check 8 | python3 -c "import sys,json; d=json.loads(sys.stdin.readline()); print(d['value'], 'ms', d['roofline']['achieved'], 'TF/s')")"
 done
 for m in mistral-7b llama-3.2-3b; do
   timeout -k 10 300 python tools/bench_small_prefill.py --model $m --ts 1,2,5,13,32,64 > $o/small_$m.txt 2>&1 || { echo "small failed"; tail -5 $o/small_$m.txt; exit 1; }

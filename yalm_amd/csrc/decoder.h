@@ -87,6 +87,7 @@ struct PfForms {
 	int g16[6] = {-1, -1, -1, -1, -1, -1}; // qkv, wo, glu, w2, cls, test
 	bool p8 = true, persist = true;
 	bool no_skinny = false; // T <= 64: split-K skinny GEMMs (prefill_skinny.h) unless set
+	bool qkv1 = true;       // the q and k | v GEMMs as ONE two-depth launch when BN 256 fits both
 };
 PfForms pf_forms_from_env();
 

@@ -22,7 +22,7 @@
 // (Llama-3B Wo / W2 N 3072 -> 192). YALM_PF_G16 = "qkv:256,wo:128,..." forces widths
 // (the exact-form tests), YALM_PF_8P=0 the 2-phase kernel, YALM_PF_PERSIST=0 one
 // workgroup per tile, YALM_PF_SKINNY=0 the large tiles at T <= 64 too (prefill_skinny.h
-// otherwise). All of them are read once, at decoder creation (PfForms); the
+// otherwise), YALM_PF_QKV1=0 the q and k | v GEMMs as two launches. All of them are read once, at decoder creation (PfForms); the
 // kernel-level test hook yalm_gemm_f16 reads them per call.
 PfForms pf_forms_from_env() {
 	static const char *names[6] = {"qkv", "wo", "glu", "w2", "cls", "test"};
@@ -40,6 +40,8 @@ PfForms pf_forms_from_env() {
 		f.persist = atoi(e) != 0;
 	if (const char *e = getenv("YALM_PF_SKINNY"))
 		f.no_skinny = atoi(e) == 0;
+	if (const char *e = getenv("YALM_PF_QKV1"))
+		f.qkv1 = atoi(e) != 0;
 	return f;
 }
 
@@ -81,9 +83,10 @@ int pick_bn(const PfForms &f, int kind, int M, int n_eff, bool glu) {
 	return best;
 }
 
+// c_split / K2: columns [c_split, N) run K2 (gemm8p_kernel); c_split = N: one depth
 template <class EPI, class BMAP, int FJ0, int FJ1>
 int launch_g8p(const PfForms &f, const uint16_t *A, int lda, int M, int K, int kb, const BMAP &bm, int N,
-               const EPI &epi, hipStream_t st, int c0) {
+               const EPI &epi, hipStream_t st, int c0, int c_split = -1, int K2 = 0) {
 	auto kern = pf::gemm8p_kernel<EPI, BMAP, FJ0, FJ1>;
 	constexpr size_t lds = pf::gemm8p_lds<FJ0, FJ1>();
 	constexpr int BN = 64 * (FJ0 + FJ1);
@@ -95,8 +98,11 @@ int launch_g8p(const PfForms &f, const uint16_t *A, int lda, int M, int K, int k
 	const int nwg = ((M + pf::G_BM - 1) / pf::G_BM) * (N / BN);
 	// more tiles than CUs: one persistent workgroup per CU walks them
 	const int ncu = (int)device_cu_count();
-	const int grid = f.persist && nwg > ncu ? ncu : nwg;
-	hipLaunchKernelGGL(kern, dim3(grid), dim3(pf::G_THREADS), lds, st, A, lda, M, K, kb, bm, N, epi, c0);
+	// (two depths: one workgroup per tile, so the hardware balances them longest first)
+	const bool two = c_split >= 0 && c_split < N;
+	const int grid = f.persist && nwg > ncu && !two ? ncu : nwg;
+	hipLaunchKernelGGL(kern, dim3(grid), dim3(pf::G_THREADS), lds, st, A, lda, M, K, kb, bm, N, epi, c0,
+	                   two ? c_split : N, two ? K2 : K);
 	HIPCHK(hipGetLastError());
 	return YALM_OK;
 }
@@ -338,6 +344,10 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 	// GEMM widths are the same for every layer
 	const int bn_q = pick_bn(f, PG_QKV, T, q_dim, false);
 	const int bn_kv = pick_bn(f, PG_QKV, T, 2 * kv_dim, false);
+	// q and k | v in one two-depth launch at width 256 (gemm8p_kernel): the two launches'
+	// tiles balanced over the chip instead of one round each (Llama-3B at T 4096: q 82 us
+	// at width 192 + k | v 115 us at 128)
+	const bool qkv1 = f.qkv1 && f.p8 && f.g16[PG_QKV] < 0 && q_dim % 256 == 0 && (2 * kv_dim) % 256 == 0;
 	const int bn_wo = pick_bn(f, PG_WO, T, c.dim, false);
 	const int bn_w2 = pick_bn(f, PG_W2, T, c.dim, false);
 	// short prompts: split-K skinny GEMMs (the 256-row tiles would leave most CUs idle)
@@ -382,8 +392,14 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 				                  st));
 				TRY(launch_skinny_reduce<false>(b.skp, ks_qkv, 2 * ks_qkv, q_dim, T, np, e, st));
 			} else {
-				TRY(launch_plain(f, bn_q, b.Xn, 2 * c.dim, T, c.dim, c.dim, qkv, q_dim, e, st));
-				TRY(launch_plain(f, bn_kv, b.Xn, 2 * c.dim, T, 2 * c.dim, c.dim, qkv, 2 * kv_dim, e, st, q_dim));
+				if (qkv1) { // one launch: the k | v tiles (K = 2 dim) first, then the q tiles (K = dim)
+					TRY((launch_g8p<pf::E16QKV, pf::BRowsPlain, 2, 2>(f, b.Xn, 2 * c.dim, T, c.dim, c.dim,
+					                                                   pf::BRowsPlain{qkv}, q_dim + 2 * kv_dim, e, st,
+					                                                   0, q_dim, 2 * c.dim)));
+				} else {
+					TRY(launch_plain(f, bn_q, b.Xn, 2 * c.dim, T, c.dim, c.dim, qkv, q_dim, e, st));
+					TRY(launch_plain(f, bn_kv, b.Xn, 2 * c.dim, T, 2 * c.dim, c.dim, qkv, 2 * kv_dim, e, st, q_dim));
+				}
 			}
 		}
 		TRY(launch_attn_prefill(b.Q, w.key_cache, w.value_cache, T, pos0, c.n_heads, c.n_kv_heads, c.head_dim, b.O,

@@ -446,9 +446,15 @@ constexpr size_t gemm16_lds() {
 //   count left in flight is the same at every phase: FJ0 + FJ1 + 4.
 constexpr int P8_HT = 128 * G_BK; // f16 per A half-tile (128 rows)
 
+// Two K depths in one launch (the QKV GEMM, §4b split-f16): columns [c_split, N) of the
+// launch run K2 (> K, the B rows wrapping at kb), columns [0, c_split) run K. Their tiles
+// (twice the work) come first in dispatch order, each class keeping its own XCD-aware
+// order: with one workgroup per tile the hardware then hands the K tiles to the CUs the
+// K2 tiles leave free (longest first).
 template <class EPI, class BMAP, int FJ0 = 2, int FJ1 = 2>
 __global__ __launch_bounds__(G_THREADS, 1) void gemm8p_kernel(const uint16_t *__restrict__ A, int lda, int M, int K,
-                                                             int kb, BMAP bm, int N, EPI epi, int c0) {
+                                                             int kb, BMAP bm, int N, EPI epi, int c0, int c_split,
+                                                             int K2) {
 	constexpr int FI = 8, FJ = FJ0 + FJ1, TM = 128, TN = 16 * FJ, BN = 4 * TN;
 	constexpr int HB0 = 64 * FJ0 * G_BK, HB1 = 64 * FJ1 * G_BK; // f16 per B half-tile
 	constexpr int OFF[4] = {0, P8_HT, 2 * P8_HT, 2 * P8_HT + HB0}; // Am0, Am1, Bn0, Bn1 in a buffer
@@ -462,18 +468,23 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm8p_kernel(const uint16_t *__
 
 	const int tiles_m = (M + G_BM - 1) / G_BM, tiles_n = N / BN;
 	const int nwg = tiles_m * tiles_n;
+	const int tn_split = c_split / BN;             // column tiles with depth K
+	const int nwg2 = tiles_m * (tiles_n - tn_split); // tiles with depth K2, dispatched first
 	// one tile per workgroup, or (grid smaller than the tile count) a persistent loop over
 	// tiles b, b + grid, ...: the next tile's LDS-DMA prologue follows this tile's epilogue
 	// stores without a workgroup exit and dispatch in between
 	for (int t = blockIdx.x; t < nwg; t += gridDim.x) {
 		if (EPI::NEEDS_LDS && t != (int)blockIdx.x) // the previous tile's epilogue is done with LDS
 			asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); // (stores may stay in flight)
-		int wg = t;
-		{
-			const int q = nwg / 8, rr = nwg % 8, xcd = wg % 8, idx = wg / 8;
+		const bool deep = t < nwg2;
+		int wg = deep ? t : t - nwg2;
+		{ // XCD-aware order inside the class: consecutive tiles of one XCD share A rows
+			const int n = deep ? nwg2 : nwg - nwg2;
+			const int q = n / 8, rr = n % 8, xcd = wg % 8, idx = wg / 8;
 			wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
 		}
-		const int tm = wg % tiles_m, tn = wg / tiles_m;
+		const int tm = wg % tiles_m, tn = wg / tiles_m + (deep ? tn_split : 0);
+		const int Kt = deep ? K2 : K;
 		const int row0 = tm * G_BM;
 		const int colB = c0 + tn * (BN / BMAP::COLS_PER_TILE_DIV); // c0: first column of this launch
 
@@ -533,7 +544,7 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm8p_kernel(const uint16_t *__
 				acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 		half8_t a[4][2], b0[FJ0][2], b1[FJ1][2];
 
-		const int nk = K / G_BK;
+		const int nk = Kt / G_BK;
 		// prologue = the previous iteration's stages p3 .. p8 for K tiles 0 (E) and 1 (O)
 		const int k1 = nk > 1 ? 1 : 0;
 		stage(0, 0, 0);
