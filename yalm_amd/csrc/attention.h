@@ -57,6 +57,54 @@ constexpr int attn_nk() {
 	return attn_chunk<D>() / (ATTN_WAVES * (64 / (D / 8))) > 0 ? attn_chunk<D>() / (ATTN_WAVES * (64 / (D / 8))) : 1;
 }
 
+// One lane's K / V rows of a 64-key chunk through buffer resources: the per-lane byte
+// offsets (row group, piece) are fixed, the chunk is a wave-uniform soffset. Rows past
+// max_seq_len (the descriptor's end) read as zeros and move no data, so a prefetch past
+// the last chunk passes soffset = end and costs nothing. Round 4 first used flat loads
+// at per-chunk 64-bit addresses: their address temporaries re-used the registers of
+// the previous chunk's loads, and hipcc drained vmcnt to 0 at every chunk-loop
+// iteration -- the next chunk's loads waited for the prefetch (one load latency per
+// two chunks).
+template <int D>
+struct KvRows {
+	static constexpr int LPK = D / 8, KPW = 64 / LPK, RSTEP = (ATTN_THREADS / 64) * KPW;
+	static constexpr int NK = attn_nk<D>();
+	__amdgpu_buffer_rsrc_t kr, vr;
+	uint32_t rowb, end;
+	uint32_t voff[NK];
+	__device__ __forceinline__ KvRows(const uint16_t *kc, const uint16_t *vc, int n_kv_heads, int max_seq_len, int g) {
+		const int lane = threadIdx.x & 63;
+		const int tl0 = (threadIdx.x >> 6) * KPW + lane / LPK, piece = lane % LPK;
+		// descriptor inputs made provably wave-uniform (readfirstlane): otherwise hipcc wraps
+		// each buffer load in a waterfall loop (cdna_hip_programming.md T20)
+		auto uni = [](const uint16_t *p) {
+			const uint64_t a = (uint64_t)p;
+			const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+			const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+			return (void *)(((uint64_t)hi << 32) | lo);
+		};
+		rowb = (uint32_t)__builtin_amdgcn_readfirstlane(n_kv_heads * D * 2);
+		end = (uint32_t)__builtin_amdgcn_readfirstlane((int)((uint32_t)max_seq_len * rowb));
+		kr = __builtin_amdgcn_make_buffer_rsrc(uni(kc), (short)0, (int)end, 0x00020000);
+		vr = __builtin_amdgcn_make_buffer_rsrc(uni(vc), (short)0, (int)end, 0x00020000);
+#pragma unroll
+		for (int i = 0; i < NK; ++i)
+			voff[i] = (uint32_t)(tl0 + i * RSTEP) * rowb + (uint32_t)(g * D + piece * 8) * 2;
+	}
+	// the chunk at row t0 (nothing when !live)
+	__device__ __forceinline__ void load(int t0, bool live, u32x4_t (&kw)[NK], u32x4_t (&vw)[NK]) const {
+		// wave-uniform (T20); t0 and live must come from scalar values (attn_core keeps its
+		// chunk loop in SGPRs): a VALU select here took a register of the previous chunk's
+		// loads and cost a vmcnt(0) per chunk
+		const uint32_t so = live ? (uint32_t)t0 * rowb : end;
+#pragma unroll
+		for (int i = 0; i < NK; ++i) {
+			kw[i] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(kr, voff[i], so, 0));
+			vw[i] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(vr, voff[i], so, 0));
+		}
+	}
+};
+
 __device__ __forceinline__ void st_sc1(float *p, float v) {
 	__hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -200,6 +248,11 @@ __device__ __forceinline__ bool attn_core(int g, int hq0, int Gh, int c_first, i
                                           unsigned ptag, float *out, float *att_dbg, unsigned gtag,
                                           unsigned long long *ts, bool trace_on) {
 	constexpr int CHUNK = attn_chunk<D>();
+	// the chunk loop's values in SGPRs (KvRows::load's soffset is computed from them)
+	c_first = __builtin_amdgcn_readfirstlane(c_first);
+	cstride = __builtin_amdgcn_readfirstlane(cstride);
+	ns = __builtin_amdgcn_readfirstlane(ns);
+	kv_len = __builtin_amdgcn_readfirstlane(kv_len);
 	constexpr int LPK = D / 8;                      // lanes per K/V row, 16 B each
 	static_assert(LPK >= 2 && LPK <= 32 && (LPK & (LPK - 1)) == 0, "head_dim 16 .. 256, a power of two");
 	constexpr int KPW = 64 / LPK;                   // row groups per wave (rows per wave-instruction)
@@ -220,15 +273,8 @@ __device__ __forceinline__ bool attn_core(int g, int hq0, int Gh, int c_first, i
 	const int piece = lane % LPK;
 	const int tl0 = wave * KPW + sub;
 
-	auto load_kv = [&](int t0, int tmax, u32x4_t (&kw)[NK], u32x4_t (&vw)[NK]) {
-#pragma unroll
-		for (int i = 0; i < NK; ++i) {
-			const int t = min(t0 + tl0 + i * RSTEP, tmax);
-			const size_t off = (size_t)t * kv_dim + g * D + piece * 8;
-			kw[i] = load16(kc + off);
-			vw[i] = load16(vc + off);
-		}
-	};
+	const KvRows<D> rows(kc, vc, n_kv_heads, max_seq_len, g);
+	auto load_kv = [&](int t0, u32x4_t (&kw)[NK], u32x4_t (&vw)[NK]) { rows.load(t0, t0 < kv_len, kw, vw); };
 	// trace (attn_wo.h, thread 0 only): s_memrealtime + shader clock (s_memtime) at
 	// checkpoint k, kept in LDS and stored at the end -- a store issued mid-way would
 	// queue behind the co-resident Wo workgroup's weight loads and stall the wave, and
@@ -447,14 +493,14 @@ __device__ __forceinline__ bool attn_core(int g, int hq0, int Gh, int c_first, i
 		chunk(T_{}, kA, vA, c_first * CHUNK);
 	} else {
 		u32x4_t kB[NK], vB[NK];
-		load_kv((c_first + cstride) * CHUNK, kv_len - 1, kB, vB);
+		load_kv((c_first + cstride) * CHUNK, kB, vB);
 		chunk(T_{}, kA, vA, c_first * CHUNK);
 		for (int c = c_first + cstride;; c += 2 * cstride) { // kB / vB hold chunk c
-			load_kv((c + cstride) * CHUNK, kv_len - 1, kA, vA);
+			load_kv((c + cstride) * CHUNK, kA, vA);
 			chunk(F_{}, kB, vB, c * CHUNK);
 			if (c + cstride >= ns)
 				break;
-			load_kv((c + 2 * cstride) * CHUNK, kv_len - 1, kB, vB);
+			load_kv((c + 2 * cstride) * CHUNK, kB, vB);
 			chunk(F_{}, kA, vA, (c + cstride) * CHUNK);
 			if (c + 2 * cstride >= ns)
 				break;
@@ -586,30 +632,19 @@ __device__ __forceinline__ bool attn_decode_body(int g, int u, int S, int head_m
 	constexpr int NK = CHUNK / RSTEP > 0 ? CHUNK / RSTEP : 1;
 	constexpr int QL = (GT * D + 255) / 256;
 	const int G = n_heads / n_kv_heads;
-	const int kv_dim = n_kv_heads * D;
 	const int lane = threadIdx.x & 63;
-	const int tl0 = (threadIdx.x >> 6) * KPW + lane / LPK;
-	const int piece = lane % LPK;
 	const bool hu = u < G;             // head unit (query head u)
 	const int s = hu ? 0 : u - G + 1; // key split
-	auto load_kv = [&](int t0, u32x4_t (&kw)[NK], u32x4_t (&vw)[NK]) {
-#pragma unroll
-		for (int i = 0; i < NK; ++i) {
-			const int t = min(t0 + tl0 + i * RSTEP, max_seq_len - 1);
-			const size_t off = (size_t)t * kv_dim + g * D + piece * 8;
-			kw[i] = load16(kc + off);
-			vw[i] = load16(vc + off);
-		}
-	};
 	// ---- speculative loads: q of the group's G heads (G * D contiguous floats, QL
-	// 16-byte pieces per lane), the unit's first chunk's K/V rows (clamped to the cache)
+	// 16-byte pieces per lane), the unit's first chunk's K/V rows (zeros past the cache)
 	const int gq = G * D;
 	float4_t qv[QL];
 #pragma unroll
 	for (int j = 0; j < QL; ++j)
 		qv[j] = *(const float4_t *)(q + (size_t)g * gq + min((j * 64 + lane) * 4, gq - 4));
 	u32x4_t kA[NK], vA[NK];
-	load_kv(s * CHUNK, kA, vA);
+	const KvRows<D> rows(kc, vc, n_kv_heads, max_seq_len, g);
+	rows.load(s * CHUNK, s * CHUNK < max_seq_len, kA, vA);
 	const int kv_len = step->kv_len;
 	const int ns = (kv_len + CHUNK - 1) / CHUNK;
 	if (ns <= head_max) { // (the host passes head_max >= 1, and >= every ns when S = 1)
