@@ -58,7 +58,6 @@ struct AttnWoArgs {
 	unsigned long long *trace; // [grid][AWO_TRACE_N] s_memrealtime stamps (YALM_ATTN_WO_TRACE=1) or null
 	int delay;          // s_memrealtime ticks (10 ns) the Wo workgroups wait before their slice loads
 	                    // (lets the attention's K/V and q loads reach HBM first)
-	bool gfirst;        // gather the head granules before polling the sentinels (awo_gather_gran)
 };
 
 // Eight 16-byte sc1 loads from arbitrary addresses in one statement, one vmcnt(0)
@@ -98,11 +97,13 @@ __device__ __forceinline__ void awo_ld8_sc1(u32x4_t (&v)[8], const void *const (
 // each covered head), then the gather. Round 3 measured a combined first attempt
 // (gather + sentinels in one round trip) slower: 1024 waves gathering the same
 // 32 KB of granules as the slices land is a burst the poll avoids
-// (profiles/r3_ab_awo.txt). False if the bounded spin gave up (deadline,
+// (profiles/r3_ab_awo.txt); round 4 measured gathering first (sentinels only after a
+// stale tag) slower again: fp8 kv 17 7.40 -> 8.49 us, kv 100 8.86 -> 11.68
+// (profiles/r4k_decode_ab.txt). False if the bounded spin gave up (deadline,
 // s_memrealtime).
 template <int EPL, int XS>
 __device__ __forceinline__ bool awo_gather_gran(float (&xs)[XS][EPL], const unsigned long long *gran, int tid,
-                                                unsigned tag, unsigned long long deadline, bool gfirst) {
+                                                unsigned tag, unsigned long long deadline) {
 	constexpr int LPP = EPL / 2;   // 16-byte loads per piece
 	constexpr int NL = XS * LPP;   // 4, 8 or 16
 	constexpr int NB = (NL + 7) / 8;
@@ -118,36 +119,6 @@ __device__ __forceinline__ bool awo_gather_gran(float (&xs)[XS][EPL], const unsi
 		sent = gran + (size_t)h * D + (D - 1);
 	}
 	asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the slice has landed
-	// gather first (round 4): with head units the heads are usually written before the
-	// slice lands (Mistral kv 17: heads at ~2.3 us, slices at ~3.2 us), so one gather
-	// round trip replaces the sentinel round trip + the gather round trip; only when a
-	// tag is stale does the wave fall back to polling the sentinels
-	if (gfirst && NB == 1) {
-		const void *a[8];
-#pragma unroll
-		for (int i = 0; i < 8; ++i) {
-			const int l = i < NL ? i : 0;
-			const int k = l / LPP, e = (l % LPP) * 2;
-			a[i] = gran + (size_t)(k * ATTN_THREADS + tid) * EPL + e;
-		}
-		u32x4_t v[8];
-		awo_ld8_sc1(v, a);
-		bool ok = true;
-#pragma unroll
-		for (int i = 0; i < 8; ++i)
-			ok = ok && v[i][1] == tag && v[i][3] == tag;
-		if (__all(ok)) {
-#pragma unroll
-			for (int i = 0; i < 8; ++i) {
-				if (i < NL) {
-					const int k = i / LPP, e = (i % LPP) * 2;
-					xs[k][e] = __uint_as_float(v[i][0]);
-					xs[k][e + 1] = __uint_as_float(v[i][2]);
-				}
-			}
-			return true;
-		}
-	}
 	for (;;) {
 		const unsigned long long g = __hip_atomic_load(sent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 		if (__all((unsigned)(g >> 32) == tag))
@@ -264,7 +235,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 	// only for the heads its columns cover), then dot them into every resident row.
 	const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 	float xs[XS][EPL];
-	if (!awo_gather_gran<EPL, XS>(xs, p.gran, tid, epoch, t0 + AWO_TIMEOUT, p.gfirst) && lane == 0)
+	if (!awo_gather_gran<EPL, XS>(xs, p.gran, tid, epoch, t0 + AWO_TIMEOUT) && lane == 0)
 		__hip_atomic_fetch_or(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 	if (tr)
 		t_poll = __builtin_amdgcn_s_memrealtime(), c_poll = __builtin_amdgcn_s_memtime();

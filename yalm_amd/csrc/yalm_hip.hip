@@ -402,8 +402,6 @@ static int attn_wo_init(yalm_decoder_s *d) {
 	// ~3.1 us, before the heads): 0.5 us gives 9.4 -> 8.4 us at kv 17, 11.3 -> 10.3 at kv 151,
 	// 579 -> 586 tok/s (profiles/r3_ab_awo_delay.txt); fp16 at 0.5 us is within noise
 	d->awo_delay = denv ? std::max(0, atoi(denv)) : (c.weight_dtype == YALM_F8E5M2 ? 50 : 20);
-	const char *genv = ab_env("YALM_AWO_GFIRST"); // A/B build: 0 = sentinel poll first (round 3)
-	d->awo_gfirst = genv ? atoi(genv) != 0 : true;
 	// Removed in round 4 (measured losers, round 3, profiles/r3_ab_awo*.txt): the combined
 	// first gather attempt (YALM_AWO_SPEC), per-XCD copies of the head outputs
 	// (YALM_AWO_REPL) and a sliding window on the Wo slice loads (YALM_ATTN_WO_WIN)
@@ -474,7 +472,6 @@ static int launch_attn_wo(yalm_decoder_s *d, const yalm_block_weights &w, int la
 	p.nsplit = attn_nsplit(c.max_seq_len);
 	p.S = d->awo_S;
 	p.head_max = attn_head_max(d->awo_S, (c.max_seq_len + attn_chunk<128>() - 1) / attn_chunk<128>());
-	p.gfirst = d->awo_gfirst;
 	p.q_dim = c.n_heads * c.head_dim;
 	p.dim = c.dim;
 	p.part = d->part;
