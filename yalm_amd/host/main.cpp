@@ -95,12 +95,12 @@ static void run_completion(const std::string &path, const std::string &device, c
 	size_t read_bytes = 0;
 	int next = 0;
 	// hydrate all but the last prompt token in one batched prefill when the
-	// model has that path (yalm_prefill) and there are at least 2 of them (one
-	// position is faster as a per-token forward: tools/bench_small_prefill.py); the
+	// model has that path (yalm_prefill) and there are at least 3 of them (one or
+	// two positions are as fast as per-token forwards: profiles/r4m_delay_prefill.txt); the
 	// last token goes through the per-token forward, which produces its logits /
 	// greedy argmax
 	size_t first = 0;
-	if (encoding.size() >= 3 && (int)encoding.size() - 1 <= model.config->max_seq_len &&
+	if (encoding.size() >= 4 && (int)encoding.size() - 1 <= model.config->max_seq_len &&
 	    model.prefill(state, encoding.data(), (int)encoding.size() - 1, 0, nullptr)) {
 		first = encoding.size() - 1;
 		for (size_t pos = 0; pos < first; ++pos)
