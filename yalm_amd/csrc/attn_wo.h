@@ -58,7 +58,6 @@ struct AttnWoArgs {
 	unsigned long long *trace; // [grid][AWO_TRACE_N] s_memrealtime stamps (YALM_ATTN_WO_TRACE=1) or null
 	int delay;          // s_memrealtime ticks (10 ns) the Wo workgroups wait before their slice loads
 	                    // (lets the attention's K/V and q loads reach HBM first)
-	int wo_early;       // Wo workgroups launched before the mergers (attn_wo_kernel: CU sharing)
 };
 
 // Eight 16-byte sc1 loads from arbitrary addresses in one statement, one vmcnt(0)
@@ -175,19 +174,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 	constexpr int EPL = WT::EPL;
 	constexpr int LPT = AWO_RPW * XS;
 	static_assert(ATTN_THREADS == 256 && ATTN_WAVES == 4, "4-wave workgroups: one 4-row reduction per wave");
-	const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-	// launch order -> role order b (attention units, mergers, Wo): the first wo_early Wo
-	// workgroups are dispatched between the attention units and the mergers, so that with
-	// a full two-per-CU grid (workgroups i and i + CUs share a CU: tools/placement_bench.hip)
-	// the mergers, not streaming Wo workgroups, share the head units' CUs
-	int b = blockIdx.x;
-	{
-		const int G0 = p.n_heads / p.n_kv, u0 = p.n_kv * (p.S + G0 - 1);
-		if (b >= u0 && b < u0 + p.wo_early)
-			b += p.n_heads; // an early Wo workgroup
-		else if (b >= u0 + p.wo_early && b < u0 + p.wo_early + p.n_heads)
-			b -= p.wo_early; // a merger
-	}
+	const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 	const int G = p.n_heads / p.n_kv;
 	const int units = p.n_kv * (p.S + G - 1); // attention workgroups (head units + split units)
 	const int munits = units + p.n_heads;     // + one merger per query head

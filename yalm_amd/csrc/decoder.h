@@ -139,7 +139,6 @@ struct yalm_decoder_s {
 	bool attn_wo = false;
 	int awo_nb = 0;                  // grid: n_kv * (awo_S + G - 1) attention + n_heads mergers + ceil(dim / AWO_RPW) Wo
 	int awo_S = 0;                   // key-chunk splits per kv head
-	int awo_wo_early = 0;            // Wo workgroups launched before the mergers (attn_wo.h)
 	unsigned long long *awo_trace = nullptr; // A/B build, YALM_ATTN_WO_TRACE=1: [grid][16] stamps of the last launch
 	int awo_delay = 0;               // ticks the Wo workgroups wait before their slice loads
 	unsigned long long *awo_gran = nullptr; // [n_layers][q_dim] attention outputs as {value, epoch} granules

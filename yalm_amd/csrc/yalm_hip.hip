@@ -395,18 +395,6 @@ static int attn_wo_init(yalm_decoder_s *d) {
 	d->awo_S = std::max(1, std::min(nchunks, senv ? std::max(1, std::min(ATTN_MAX_SPLITS, atoi(senv)))
 	                                                : std::min(ATTN_SPLITS, fit)));
 	d->awo_nb = c.n_kv_heads * (d->awo_S + G - 1) + c.n_heads + n_wo;
-	// Workgroups i and i + CUs of a two-per-CU grid share a CU (tools/placement_bench.hip:
-	// 256 of 256 on MI355X). Launched in role order, the head units (launch indices < n_heads)
-	// shared their CUs with the first Wo workgroups, and the slice loads queued ahead of the
-	// head units' output stores held them ~1 us (P.V -> signal 1.6 us, 0.6 with the slices
-	// delayed past them: profiles/r4m_*). So the first wo_early Wo workgroups launch before
-	// the mergers, which then start at launch index CUs, next to the head units; they exit
-	// at once in head mode and only poll in key mode. (Every wait still points at workgroups
-	// that wait on nothing but earlier roles: attention units never wait, mergers wait on
-	// attention units, Wo on both; an early Wo workgroup spinning holds one slot.)
-	const int units = c.n_kv_heads * (d->awo_S + G - 1);
-	const char *eenv = ab_env("YALM_AWO_EARLY"); // A/B build: 0 = role order
-	d->awo_wo_early = (eenv && atoi(eenv) == 0) ? 0 : std::max(0, std::min(n_wo, device_cu_count() - units));
 	const char *denv = ab_env("YALM_ATTN_WO_DELAY");
 	// default 0.2 us (fp16) / 0.5 us (fp8): the attention workgroups' K/V loads reach HBM
 	// ahead of the Wo stream. fp16 (33.5 MB, slice lands ~5.4 us, after the heads):
@@ -484,7 +472,6 @@ static int launch_attn_wo(yalm_decoder_s *d, const yalm_block_weights &w, int la
 	p.nsplit = attn_nsplit(c.max_seq_len);
 	p.S = d->awo_S;
 	p.head_max = attn_head_max(d->awo_S, (c.max_seq_len + attn_chunk<128>() - 1) / attn_chunk<128>());
-	p.wo_early = d->awo_wo_early;
 	p.q_dim = c.n_heads * c.head_dim;
 	p.dim = c.dim;
 	p.part = d->part;
