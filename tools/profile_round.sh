@@ -13,10 +13,10 @@ mkdir -p $out
 dtypes="${@:-fp16 fp8}"
 for dt in $dtypes; do
   YALM_EAGER=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace_$dt -o bench -- \
-    python3 bench.py --steps 64 --warmup 4 --no-cpu-baseline --no-gpu-state --no-prefill --no-fp8 --dtype $dt > $out/trace_bench_$dt.log 2>&1
+    python3 bench.py --steps 64 --warmup 4 --no-cpu-baseline --no-gpu-state --no-prefill --no-fp8 --no-long --dtype $dt > $out/trace_bench_$dt.log 2>&1
   echo "trace $dt ok"
   YALM_EAGER=1 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/pmc_$dt -o pmc -- \
-    python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline --no-gpu-state --no-prefill --no-fp8 --no-envelope --kernel-iters 8 --dtype $dt \
+    python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline --no-gpu-state --no-prefill --no-fp8 --no-long --no-envelope --kernel-iters 8 --dtype $dt \
     > $out/pmc_bench_$dt.log 2>&1
   echo "pmc $dt ok"
 done
