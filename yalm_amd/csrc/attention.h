@@ -602,9 +602,8 @@ __device__ __forceinline__ bool attn_core(int g, int hq0, int Gh, int c_first, i
 
 // One attention workgroup: unit u of kv head g's S + G - 1 units. Units u < G are HEAD
 // units (query head u of the group), units u >= G are SPLIT units (every query head of
-// the group, key split s = u - G + 1). Speculative loads first (q, the unit's first
-// chunk, which is known before kv_len: chunk 0 for a head unit, chunk s for a split
-// unit), then one of
+// the group, key split s = u - G + 1). Speculative loads first (q; a head unit's first
+// chunk, chunk 0 in both modes), then one of
 //   * HEAD mode (kv_len <= head_max chunks): head unit u runs query head u over ALL
 //     the chunks and writes it directly -- no partial, no merger hop, and a quarter of
 //     the per-wave arithmetic of a 4-head chunk (Mistral: G = 4). The G head units of a
@@ -642,9 +641,15 @@ __device__ __forceinline__ bool attn_decode_body(int g, int u, int S, int head_m
 #pragma unroll
 	for (int j = 0; j < QL; ++j)
 		qv[j] = *(const float4_t *)(q + (size_t)g * gq + min((j * 64 + lane) * 4, gq - 4));
+	// head units: chunk 0, speculatively; split units load their chunk once kv_len says it
+	// holds keys (their speculative loads were 6.3 MB of dead reads per layer at short
+	// contexts, 192 units x 32 KB: fused fp8 kv 17 8.3 -> 7.9 us, fp16 bench +0.9%, long
+	// context -0.2%, profiles/r4q_split_spec.txt). The instruction stays unconditional
+	// (a split unit's passes the descriptor's end and moves no data): hipcc's vmcnt
+	// counting stays static.
 	u32x4_t kA[NK], vA[NK];
 	const KvRows<D> rows(kc, vc, n_kv_heads, max_seq_len, g);
-	rows.load(s * CHUNK, s * CHUNK < max_seq_len, kA, vA);
+	rows.load(0, hu, kA, vA);
 	const int kv_len = step->kv_len;
 	const int ns = (kv_len + CHUNK - 1) / CHUNK;
 	if (ns <= head_max) { // (the host passes head_max >= 1, and >= every ns when S = 1)
@@ -655,6 +660,8 @@ __device__ __forceinline__ bool attn_decode_body(int g, int u, int S, int head_m
 	}
 	if (s * CHUNK >= kv_len)
 		return false;
+	if (!hu)
+		rows.load(s * CHUNK, true, kA, vA);
 	// key mode: ns >= 2 and S >= 2, so every head has at least two partials and the
 	// mergers write the heads
 	if (hu)
