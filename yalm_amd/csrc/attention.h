@@ -13,9 +13,10 @@
 // trips: K/V rows are read as 16-byte pieces (D/8 lanes per row); the
 // cross-lane sums go through LDS (shuffles lower to serialised ds_bpermute
 // round trips on gfx950) and the softmax reductions use DPP; chunks are
-// small (64 keys) so the KV read spreads over many CUs, and all K, V and q
-// loads are issued speculatively before kv_len is known (rows past kv_len are
-// read but masked), overlapping the step-state load.
+// small (64 keys) so the KV read spreads over many CUs, and the q and first
+// K/V chunk loads of the per-head workgroups are issued speculatively before
+// kv_len is known (rows past kv_len are read but masked), overlapping the
+// step-state load.
 //  * Short contexts (<= ATTN_HEAD_MAX chunks, "head mode"): one workgroup per
 //    query head runs all the keys and writes the head directly.
 //  * Longer contexts ("key mode"): the keys are split over S key splits per kv
