@@ -286,6 +286,7 @@ def prefill_leg(runtime, M, model="llama-3.2-3b", n=4096, iters=3, check=48):
     tests/test_gpu_prefill_llama.py)."""
     import numpy as np
 
+    check = max(1, check)
     cfg = M.PRESETS[model].with_(weight_dtype=M.F16, max_seq_len=max(n, 64))
     q_dim, kv_dim = cfg.n_heads * cfg.head_dim, cfg.n_kv_heads * cfg.head_dim
     gemm = 2 * n * (cfg.dim * (q_dim + 2 * kv_dim) + q_dim * cfg.dim + 3 * cfg.dim * cfg.hidden_dim)
