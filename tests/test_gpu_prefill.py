@@ -206,9 +206,13 @@ def test_prefill_short_prompt_paths(cfg_name, n, monkeypatch):
     monkeypatch.setenv("YALM_PF_SKINNY", "0")
     dec_l = R.Decoder(dm)
     monkeypatch.delenv("YALM_PF_SKINNY")
+    monkeypatch.setenv("YALM_PF_SKL", "0")  # the skinny GEMMs' weights as register loads
+    dec_r = R.Decoder(dm)
+    monkeypatch.delenv("YALM_PF_SKL")
     dec_d = R.Decoder(dm)
     try:
-        lp_s, lp_l = dec_s.prefill(tokens), dec_l.prefill(tokens)
+        lp_s, lp_l, lp_r = dec_s.prefill(tokens), dec_l.prefill(tokens), dec_r.prefill(tokens)
+        np.testing.assert_array_equal(lp_s, lp_r)  # LDS-DMA or register weights: the same MFMA sequence
         np.testing.assert_allclose(lp_s, lp_l, atol=2e-3)  # the same f16 operands, another f32 sum order
         if n > 1:
             assert np.max(np.abs(lp_s[: n - 1] - _decode_logprobs(dec_d, tokens))) <= LP_ATOL
@@ -219,6 +223,7 @@ def test_prefill_short_prompt_paths(cfg_name, n, monkeypatch):
     finally:
         dec_s.close()
         dec_l.close()
+        dec_r.close()
         dec_d.close()
         dm.close()
 

@@ -22,7 +22,8 @@
 // (Llama-3B Wo / W2 N 3072 -> 192). YALM_PF_G16 = "qkv:256,wo:128,..." forces widths
 // (the exact-form tests), YALM_PF_8P=0 the 2-phase kernel, YALM_PF_PERSIST=0 one
 // workgroup per tile, YALM_PF_SKINNY=0 the large tiles at T <= 64 too (prefill_skinny.h
-// otherwise), YALM_PF_QKV1=0 the q and k | v GEMMs as two launches. All of them are read once, at decoder creation (PfForms); the
+// otherwise), YALM_PF_QKV1=0 the q and k | v GEMMs as two launches, YALM_PF_SKL=0 the
+// skinny GEMMs' weights as register loads instead of LDS-DMA stages. All of them are read once, at decoder creation (PfForms); the
 // kernel-level test hook yalm_gemm_f16 reads them per call.
 PfForms pf_forms_from_env() {
 	static const char *names[6] = {"qkv", "wo", "glu", "w2", "cls", "test"};
@@ -42,6 +43,8 @@ PfForms pf_forms_from_env() {
 		f.no_skinny = atoi(e) == 0;
 	if (const char *e = getenv("YALM_PF_QKV1"))
 		f.qkv1 = atoi(e) != 0;
+	if (const char *e = getenv("YALM_PF_SKL"))
+		f.skl = atoi(e) != 0;
 	return f;
 }
 
@@ -174,7 +177,7 @@ int sk_pick_ks(std::initializer_list<SkGemm> kn, int TP) {
 		bool ok = true;
 		for (auto &p : kn) {
 			const int s = ks * p.mult;
-			ok = ok && p.K % s == 0 && (p.K / s) % pf::SK_KSTEP == 0 && (size_t)TP * (p.K / s) * 2 <= 65536;
+			ok = ok && p.K % s == 0 && (p.K / s) % pf::SK_KSTEP == 0 && (size_t)TP * (p.K / s) * 2 <= 32768;
 		}
 		if (!ok)
 			continue;
@@ -186,16 +189,17 @@ int sk_pick_ks(std::initializer_list<SkGemm> kn, int TP) {
 }
 
 template <int MT, class BMAP>
-int launch_skinny_mt(const uint16_t *A, int lda, int T, int K, int kb, const BMAP &bm, int N, int KS, int c0, int Np,
-                     float *part, hipStream_t st) {
-	auto kern = pf::skinny_gemm_kernel<MT, BMAP>;
-	static bool attr = false;
-	if (!attr) {
-		HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
-		attr = true;
+int launch_skinny_mt(const PfForms &f, const uint16_t *A, int lda, int T, int K, int kb, const BMAP &bm, int N,
+                     int KS, int c0, int Np, float *part, hipStream_t st) {
+	auto kern = f.skl ? pf::skinny_gemm_lds_kernel<MT, BMAP> : pf::skinny_gemm_kernel<MT, BMAP>;
+	static bool attr[2] = {false, false};
+	if (!attr[f.skl]) {
+		HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+		                           32768 + (int)pf::SKL_RING_BYTES));
+		attr[f.skl] = true;
 	}
 	const int KC = K / KS;
-	const size_t lds = (size_t)16 * MT * KC * sizeof(uint16_t);
+	const size_t lds = (size_t)16 * MT * KC * sizeof(uint16_t) + (f.skl ? pf::SKL_RING_BYTES : 0);
 	hipLaunchKernelGGL(kern, dim3((N / pf::SK_ROWS) * KS), dim3(256), lds, st, A, lda, T, K, kb, bm, N, KC, c0, Np,
 	                   part);
 	HIPCHK(hipGetLastError());
@@ -203,17 +207,17 @@ int launch_skinny_mt(const uint16_t *A, int lda, int T, int K, int kb, const BMA
 }
 
 template <class BMAP>
-int launch_skinny(const uint16_t *A, int lda, int T, int K, int kb, const BMAP &bm, int N, int KS, int c0, int Np,
-                  float *part, hipStream_t st) {
+int launch_skinny(const PfForms &f, const uint16_t *A, int lda, int T, int K, int kb, const BMAP &bm, int N, int KS,
+                  int c0, int Np, float *part, hipStream_t st) {
 	switch ((T + 15) / 16) {
 	case 1:
-		return launch_skinny_mt<1>(A, lda, T, K, kb, bm, N, KS, c0, Np, part, st);
+		return launch_skinny_mt<1>(f, A, lda, T, K, kb, bm, N, KS, c0, Np, part, st);
 	case 2:
-		return launch_skinny_mt<2>(A, lda, T, K, kb, bm, N, KS, c0, Np, part, st);
+		return launch_skinny_mt<2>(f, A, lda, T, K, kb, bm, N, KS, c0, Np, part, st);
 	case 3:
-		return launch_skinny_mt<3>(A, lda, T, K, kb, bm, N, KS, c0, Np, part, st);
+		return launch_skinny_mt<3>(f, A, lda, T, K, kb, bm, N, KS, c0, Np, part, st);
 	default:
-		return launch_skinny_mt<4>(A, lda, T, K, kb, bm, N, KS, c0, Np, part, st);
+		return launch_skinny_mt<4>(f, A, lda, T, K, kb, bm, N, KS, c0, Np, part, st);
 	}
 }
 
@@ -387,8 +391,8 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 			if (small) {
 				const pf::BRowsPlain bm{qkv};
 				const int np = q_dim + 2 * kv_dim;
-				TRY(launch_skinny(b.Xn, 2 * c.dim, T, c.dim, c.dim, bm, q_dim, ks_qkv, 0, np, b.skp, st));
-				TRY(launch_skinny(b.Xn, 2 * c.dim, T, 2 * c.dim, c.dim, bm, 2 * kv_dim, 2 * ks_qkv, q_dim, np, b.skp,
+				TRY(launch_skinny(f, b.Xn, 2 * c.dim, T, c.dim, c.dim, bm, q_dim, ks_qkv, 0, np, b.skp, st));
+				TRY(launch_skinny(f, b.Xn, 2 * c.dim, T, 2 * c.dim, c.dim, bm, 2 * kv_dim, 2 * ks_qkv, q_dim, np, b.skp,
 				                  st));
 				TRY(launch_skinny_reduce<false>(b.skp, ks_qkv, 2 * ks_qkv, q_dim, T, np, e, st));
 			} else {
@@ -410,7 +414,7 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 			e.ldx = c.dim;
 			e.M = T;
 			if (small) {
-				TRY(launch_skinny(b.O, q_dim, T, q_dim, q_dim, pf::BRowsPlain{one(w.wo, c.dim)}, c.dim, ks_wo, 0, c.dim,
+				TRY(launch_skinny(f, b.O, q_dim, T, q_dim, q_dim, pf::BRowsPlain{one(w.wo, c.dim)}, c.dim, ks_wo, 0, c.dim,
 				                  b.skp, st));
 				TRY(launch_skinny_reduce<false>(b.skp, ks_wo, ks_wo, c.dim, T, c.dim, e, st));
 			} else {
@@ -421,7 +425,7 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 		HIPCHK(hipGetLastError());
 		if (small) {
 			const pf::BRowsGlu<64> bm{(const uint16_t *)w.w1, (const uint16_t *)w.w3};
-			TRY(launch_skinny(b.Xn, c.dim, T, c.dim, c.dim, bm, 2 * c.hidden_dim, ks_glu, 0, 2 * c.hidden_dim, b.skp,
+			TRY(launch_skinny(f, b.Xn, c.dim, T, c.dim, c.dim, bm, 2 * c.hidden_dim, ks_glu, 0, 2 * c.hidden_dim, b.skp,
 			                  st));
 			if (c.act == YALM_SILU) {
 				pf::E16Glu<1> e;
@@ -441,7 +445,7 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 			e.ldx = c.dim;
 			e.M = T;
 			if (small) {
-				TRY(launch_skinny(b.H, c.hidden_dim, T, c.hidden_dim, c.hidden_dim, pf::BRowsPlain{one(w.w2, c.dim)},
+				TRY(launch_skinny(f, b.H, c.hidden_dim, T, c.hidden_dim, c.hidden_dim, pf::BRowsPlain{one(w.w2, c.dim)},
 				                  c.dim, ks_w2, 0, c.dim, b.skp, st));
 				TRY(launch_skinny_reduce<false>(b.skp, ks_w2, ks_w2, c.dim, T, c.dim, e, st));
 			} else {

@@ -34,6 +34,34 @@ __device__ __forceinline__ half8_t sk_afrag(const uint16_t *lds, int KC, int row
 	return *(const half8_t *)(lds + (size_t)row * KC + 8 * c);
 }
 
+// A rows [0, TP) x columns [k0, k0 + KC) into LDS, 16-byte chunk c of row r at c ^ (r & 15)
+// (rows past T are zeros). TP * KC <= 16384 f16 (32 KB: the host's K split) = at most
+// SK_AMAX chunks per thread, all loaded before any is stored: one memory round trip.
+// (A loop of load -> LDS store per chunk waited vmcnt(0) per chunk -- and for the weight
+// loads issued before it: 8 serial round trips per workgroup.)
+constexpr int SK_AMAX = 8;
+template <int MT>
+__device__ __forceinline__ void sk_stage_a(uint16_t *as, const uint16_t *__restrict__ A, int lda, int T, int k0,
+                                           int KC) {
+	constexpr int TP = 16 * MT;
+	const int cpr = KC / 8, nch = TP * cpr, tid = threadIdx.x;
+	u32x4_t v[SK_AMAX];
+#pragma unroll
+	for (int u = 0; u < SK_AMAX; ++u) {
+		const int i = min(tid + 256 * u, nch - 1);
+		const int r = i / cpr, c = i % cpr;
+		v[u] = *(const u32x4_t *)(A + (size_t)min(r, T - 1) * lda + k0 + 8 * c);
+	}
+#pragma unroll
+	for (int u = 0; u < SK_AMAX; ++u) {
+		const int i = tid + 256 * u;
+		if (i < nch) {
+			const int r = i / cpr, c = i % cpr;
+			*(u32x4_t *)(as + (size_t)r * KC + 8 * (c ^ (r & 15))) = r < T ? v[u] : u32x4_t{0u, 0u, 0u, 0u};
+		}
+	}
+}
+
 // C[:, c0 .. c0 + N) partials over K columns of A (row stride lda; B rows kb wide,
 // wrapping), K chunks of KC: part[ks][row][c] with row stride Np (c absolute).
 template <int MT, class BMAP>
@@ -65,15 +93,7 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(const uint16_t *__rest
 #pragma unroll
 	for (int u = 0; u < SK_U; ++u)
 		b[u] = __builtin_bit_cast(half8_t, load_nt16(wrow + 32 * (u < nst ? u : 0)));
-	// ---- A rows [0, TP) x columns [k0, k0 + KC) into LDS (rows past T are zeros)
-	const int cpr = KC / 8; // 16-byte chunks per row
-	for (int i = tid; i < TP * cpr; i += 256) {
-		const int r = i / cpr, c = i % cpr;
-		u32x4_t v = u32x4_t{0u, 0u, 0u, 0u};
-		if (r < T)
-			v = *(const u32x4_t *)(A + (size_t)r * lda + k0 + 8 * c);
-		*(u32x4_t *)(as + (size_t)r * KC + 8 * (c ^ (r & 15))) = v;
-	}
+	sk_stage_a<MT>(as, A, lda, T, k0, KC);
 	__syncthreads();
 	f32x4_t acc[MT];
 #pragma unroll
@@ -100,6 +120,86 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(const uint16_t *__rest
 #pragma unroll
 		for (int r = 0; r < 4; ++r)
 			pp[(size_t)(16 * m + crow16(r, lane)) * Np + col + (lane & 15)] = acc[m][r];
+}
+
+// The same partials with the weight rows staged through LDS by LDS-DMA, so every
+// wave-instruction reads 4 rows x 256 contiguous bytes (skinny_gemm_kernel's register
+// loads read 16 rows x 64 B per instruction: half cache lines, 16 DRAM rows at once).
+// Each wave owns its 16 weight rows in a 3-stage ring of 128-column stages (4 KB per
+// wave per stage): no workgroup barrier in the loop, one counted vmcnt per stage. The
+// 16-byte chunks of a row are XOR-swizzled by the row (source side of the DMA) so the
+// MFMA B-fragment reads (16 rows x one chunk) spread over the banks. LDS: the A chunk
+// (<= 32 KB) + 48 KB of ring: two workgroups per CU.
+constexpr int SKL_KS = 128;                    // K columns per stage
+constexpr int SKL_NS = 3;                      // ring stages
+constexpr int SKL_STAGE = SK_ROWS * SKL_KS;    // f16 per stage (16 KB)
+constexpr size_t SKL_RING_BYTES = (size_t)SKL_NS * SKL_STAGE * 2;
+
+template <int MT, class BMAP>
+__global__ __launch_bounds__(256) void skinny_gemm_lds_kernel(const uint16_t *__restrict__ A, int lda, int T, int K,
+                                                              int kb, BMAP bm, int N, int KC, int c0, int Np,
+                                                              float *__restrict__ part) {
+	extern __shared__ __attribute__((aligned(16))) uint16_t sm[];
+	constexpr int TP = 16 * MT;
+	uint16_t *const as = sm;                                      // [TP][KC], swizzled as skinny_gemm_kernel
+	uint16_t *const ring = sm + (size_t)TP * KC;                  // [SKL_NS][64 rows][SKL_KS]
+	const int nblk = N / SK_ROWS;
+	const int nb = blockIdx.x % nblk, ks = blockIdx.x / nblk;
+	const int k0 = ks * KC;
+	const int tid = threadIdx.x, lane = tid & 63;
+	const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+	const int cb = c0 + nb * SK_ROWS;      // the workgroup's first B row (output column)
+	const int col = cb + 16 * wave;        // the wave's
+	const int kw0 = k0 < kb ? k0 : k0 - kb; // B wrap (a K chunk never straddles kb)
+	const int nst = KC / SKL_KS;
+	// DMA geometry: instruction i of a stage covers the wave's rows 4 i .. 4 i + 3, lane
+	// l row 4 i + (l >> 4), LDS slot l & 15 <- source chunk (l & 15) ^ row
+	const uint16_t *src[4];
+#pragma unroll
+	for (int i = 0; i < 4; ++i) {
+		const int rr = 4 * i + (lane >> 4);
+		src[i] = bm.row(cb / BMAP::COLS_PER_TILE_DIV, 16 * wave + rr, kb) + kw0 + 8 * ((lane & 15) ^ rr);
+	}
+	uint16_t *const wring = ring + wave * 16 * SKL_KS; // this wave's rows in every stage
+	auto issue = [&](int st) { // stage st (clamped: past the chunk it re-reads the last stage, an L2 hit)
+		const int sc = st < nst ? st : nst - 1;
+		uint16_t *dst = wring + (st % SKL_NS) * SKL_STAGE;
+#pragma unroll
+		for (int i = 0; i < 4; ++i)
+			__builtin_amdgcn_global_load_lds((const void *)(src[i] + sc * SKL_KS),
+			                                 (YALM_LDS void *)(dst + 4 * i * SKL_KS), 16, 0, 0);
+	};
+	issue(0);
+	issue(1);
+	sk_stage_a<MT>(as, A, lda, T, k0, KC);
+	__syncthreads();
+	f32x4_t acc[MT];
+#pragma unroll
+	for (int m = 0; m < MT; ++m)
+		acc[m] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+	const int n = lane & 15, q = lane >> 4;
+	for (int st = 0; st < nst; ++st) {
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // stage st - 1's B reads are done...
+		issue(st + 2); // ...before its slot is re-staged
+		asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); // stage st landed (2 stages x 4 behind it)
+		const uint16_t *bst = wring + (st % SKL_NS) * SKL_STAGE + n * SKL_KS;
+#pragma unroll
+		for (int j = 0; j < SKL_KS / 32; ++j) {
+			const half8_t b = *(const half8_t *)(bst + 8 * ((4 * j + q) ^ n));
+#pragma unroll
+			for (int m = 0; m < MT; ++m) {
+				const half8_t a = sk_afrag<MT>(as, KC, 16 * m + n, st * SKL_KS + 32 * j + 8 * q);
+				acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, acc[m], 0, 0, 0);
+			}
+		}
+	}
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the clamped tail stages, before the wave exits
+	float *pp = part + (size_t)ks * TP * Np;
+#pragma unroll
+	for (int m = 0; m < MT; ++m)
+#pragma unroll
+		for (int r = 0; r < 4; ++r)
+			pp[(size_t)(16 * m + crow16(r, lane)) * Np + col + n] = acc[m][r];
 }
 
 // One wave per (16 rows, 16 FJ columns) block of C: the KS partials summed
