@@ -46,7 +46,7 @@ PfForms pf_forms_from_env() {
 	if (const char *e = getenv("YALM_PF_SKL"))
 		f.skl = atoi(e) != 0;
 	if (const char *e = getenv("YALM_PF_AKT"))
-		f.akt = atoi(e) == 32 ? 32 : 64;
+		f.akt = atoi(e) == 32 || atoi(e) == 33 ? atoi(e) : 64;
 	return f;
 }
 
@@ -241,29 +241,34 @@ pf::BSrc one(const void *w, int rows) {
 	return b;
 }
 
-template <int D, int KT>
+template <int D, int KT, int NST = 2>
 int launch_attn_prefill_t(const dim3 &grid, const uint16_t *Q, const uint16_t *kc, const uint16_t *vc, int T,
-                           int pos0, int n_heads, int n_kv, uint16_t *O, hipStream_t st) {
+                          int pos0, int n_heads, int n_kv, uint16_t *O, hipStream_t st) {
 	static bool attr = false;
 	if (!attr) {
-		HIPCHK(hipFuncSetAttribute((const void *)pf::attn_prefill_kernel<D, KT>,
-		                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)pf::attn_prefill_lds<D, KT>()));
+		HIPCHK(hipFuncSetAttribute((const void *)pf::attn_prefill_kernel<D, KT, NST>,
+		                           hipFuncAttributeMaxDynamicSharedMemorySize,
+		                           (int)pf::attn_prefill_lds<D, KT, NST>()));
 		attr = true;
 	}
-	pf::attn_prefill_kernel<D, KT><<<grid, pf::THREADS, pf::attn_prefill_lds<D, KT>(), st>>>(Q, kc, vc, T, pos0,
-	                                                                                         n_heads, n_kv, O);
+	pf::attn_prefill_kernel<D, KT, NST><<<grid, pf::THREADS, pf::attn_prefill_lds<D, KT, NST>(), st>>>(
+	    Q, kc, vc, T, pos0, n_heads, n_kv, O);
 	return YALM_OK;
 }
 
 // kt: keys per tile (64, or 32: half the LDS and 158 instead of 175 VGPRs at head_dim 128,
-// three workgroups per CU instead of two)
+// three workgroups per CU instead of two; 33: 32-key tiles in 3 stages)
 int launch_attn_prefill(const uint16_t *Q, const uint16_t *kc, const uint16_t *vc, int T, int pos0, int n_heads,
                         int n_kv, int head_dim, uint16_t *O, hipStream_t st, int kt) {
 	const dim3 grid(n_heads, (T + pf::AQ - 1) / pf::AQ); // heads fastest: longest-first dispatch
-	if (head_dim == 128 && kt == 32)
+	if (head_dim == 128 && kt == 33)
+		TRY((launch_attn_prefill_t<128, 32, 3>(grid, Q, kc, vc, T, pos0, n_heads, n_kv, O, st)));
+	else if (head_dim == 128 && kt == 32)
 		TRY((launch_attn_prefill_t<128, 32>(grid, Q, kc, vc, T, pos0, n_heads, n_kv, O, st)));
 	else if (head_dim == 128)
 		TRY((launch_attn_prefill_t<128, 64>(grid, Q, kc, vc, T, pos0, n_heads, n_kv, O, st)));
+	else if (head_dim == 64 && kt == 33)
+		TRY((launch_attn_prefill_t<64, 32, 3>(grid, Q, kc, vc, T, pos0, n_heads, n_kv, O, st)));
 	else if (head_dim == 64 && kt == 32)
 		TRY((launch_attn_prefill_t<64, 32>(grid, Q, kc, vc, T, pos0, n_heads, n_kv, O, st)));
 	else if (head_dim == 64)
