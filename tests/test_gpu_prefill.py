@@ -46,7 +46,7 @@ def test_gemm_exact_integers(M_, N, K):
 # one workgroup per tile instead of the persistent tile loop. The round-2 128 x 128
 # kernel and its stage / wide forms were removed in round 4.
 G16_ALL = "qkv:{0},wo:{0},glu:{0},w2:{0},cls:{0},test:{0}"
-FORMS = {"auto": {}, "auto-qkv2": {"YALM_PF_QKV1": "0"}, "auto-akt32": {"YALM_PF_AKT": "32"}, "auto-akt33": {"YALM_PF_AKT": "33"},
+FORMS = {"auto": {}, "auto-qkv2": {"YALM_PF_QKV1": "0"},
          "g16-256": {"YALM_PF_G16": G16_ALL.format(256)},
          "g16-256-2ph": {"YALM_PF_G16": G16_ALL.format(256), "YALM_PF_8P": "0"}, "g16-128": {"YALM_PF_G16": G16_ALL.format(128)},
          "g16-192": {"YALM_PF_G16": G16_ALL.format(192)},
@@ -103,11 +103,9 @@ def _attn_ref(q, kc, vc, T, pos0, nh, nkv, D):
     return out.reshape(T, nh * D)
 
 
-@pytest.mark.parametrize("akt", ["64", "32", "33"])
 @pytest.mark.parametrize("T,pos0", [(1, 0), (37, 0), (128, 0), (200, 0), (70, 50)])
 @pytest.mark.parametrize("nh,nkv,D", [(8, 2, 64), (4, 4, 128), (6, 2, 128)])
-def test_attn_prefill(T, pos0, nh, nkv, D, akt, monkeypatch):
-    monkeypatch.setenv("YALM_PF_AKT", akt)  # keys per tile (33: 32 in 3 LDS stages)
+def test_attn_prefill(T, pos0, nh, nkv, D):
     rng = np.random.default_rng(T * 31 + pos0 + D)
     q = rng.standard_normal((T, nh * D)).astype(np.float16)
     kc = rng.standard_normal((pos0 + T, nkv * D)).astype(np.float16)
@@ -140,7 +138,7 @@ CFGS = {
 
 
 @pytest.mark.parametrize("cfg_name", ["gqa-d128", "d768"])
-@pytest.mark.parametrize("form", ["auto", "auto-qkv2", "auto-akt32", "auto-akt33", "g16-256", "g16-256-2ph", "g16-128", "g16-128-2ph", "g16-192",
+@pytest.mark.parametrize("form", ["auto", "auto-qkv2", "g16-256", "g16-256-2ph", "g16-128", "g16-128-2ph", "g16-192",
                                   "g16-192-2ph", "g16-320", "g16-256-nopersist"])
 def test_prefill_forms_match_decode(form, cfg_name, monkeypatch):
     """The whole prefill in each GEMM form (incl. the vocab-tiled logits epilogue, the

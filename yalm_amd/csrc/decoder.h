@@ -89,7 +89,6 @@ struct PfForms {
 	bool no_skinny = false; // T <= 64: split-K skinny GEMMs (prefill_skinny.h) unless set
 	bool qkv1 = true;       // the q and k | v GEMMs as ONE two-depth launch when BN 256 fits both
 	bool skl = true;        // skinny GEMMs: weight rows staged by LDS-DMA (prefill_skinny.h)
-	int akt = 64;           // causal attention: keys per tile (64, 32, or 33 = 32 in 3 LDS stages)
 };
 PfForms pf_forms_from_env();
 

@@ -75,10 +75,10 @@ __device__ __forceinline__ void raw_barrier() {
 //   its B fragments are row reads)
 constexpr int AQ = 128, AKT = 64; // queries per workgroup, keys per tile
 
-// Dynamic LDS of attn_prefill_kernel<D, KT, NST>: K[NST][KT][D], V[NST][KT][D] (f16).
-template <int D, int KT = AKT, int NST = 2>
+// Dynamic LDS of attn_prefill_kernel<D, KT>: K[2][KT][D], V[2][KT][D] (f16).
+template <int D, int KT = AKT>
 constexpr size_t attn_prefill_lds() {
-	return (size_t)(2 * NST * KT * D) * 2;
+	return (size_t)(4 * KT * D) * 2;
 }
 
 // Stage one 64-key tile of K or V (rows key0.., kv head g) by LDS-DMA. Row r of
@@ -113,23 +113,18 @@ typedef short short4_t __attribute__((ext_vector_type(4)));
 // 16 s + 8 (e >> 2) + 4 h + (e & 3) of the 32-key block) with V^T fragments
 // from hardware-transposed LDS reads. O^T keeps the query on the lane too, so
 // the online-softmax rescale is one per-lane factor.
-// NST: K/V stages in LDS. 2: the next tile's DMA overlaps this tile's math, one
-// vmcnt(0) + barrier per tile. 3: two tiles in flight (counted vmcnt), a barrier before
-// a stage is restaged and one after it has landed.
-template <int D, int KT = AKT, int NST = 2>
+template <int D, int KT = AKT>
 __global__ __launch_bounds__(THREADS) void attn_prefill_kernel(const uint16_t *__restrict__ Q,
                                                                const uint16_t *__restrict__ kc,
                                                                const uint16_t *__restrict__ vc, int T, int pos0,
                                                                int n_heads, int n_kv, uint16_t *__restrict__ O) {
 	static_assert(D == 64 || D == 128, "head_dim");
 	static_assert(KT == 32 || KT == 64, "keys per tile");
-	static_assert(NST == 2 || NST == 3, "stages");
 	constexpr int NJ = KT / 32; // 32-key blocks per tile
 	constexpr int DCH = D / 8;
-	constexpr int PER = 2 * (KT / (1024 / (D * 2)) / 4); // LDS-DMA instructions per wave per stage (K + V)
 	extern __shared__ __attribute__((aligned(16))) uint16_t asmem[];
-	uint16_t *const Kb = asmem;                 // [NST][KT * D]
-	uint16_t *const Vb = asmem + NST * KT * D; // [NST][KT * D]
+	uint16_t *const Kb = asmem;               // [2][KT * D]
+	uint16_t *const Vb = asmem + 2 * KT * D; // [2][KT * D]
 	const int lane = threadIdx.x & 63, l32 = lane & 31, hh = lane >> 5;
 	const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 	// grid (heads, query blocks), x fastest: every head's heaviest (latest) query block
@@ -162,30 +157,16 @@ __global__ __launch_bounds__(THREADS) void attn_prefill_kernel(const uint16_t *_
 	const int gi = lane & 15, gq = gi >> 2, gp = gi & 3;
 	const int dgrp = 16 * ((lane >> 4) & 1);
 
-	auto stage = [&](int buf, int tile) {
-		stage_kv<D, false, KT>(Kb + buf * KT * D, kc, tile * KT, kv_rows, kv_dim, g, wave, lane);
-		stage_kv<D, true, KT>(Vb + buf * KT * D, vc, tile * KT, kv_rows, kv_dim, g, wave, lane);
-	};
-	stage(0, 0);
-	if constexpr (NST == 2) {
-		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-		__syncthreads();
-	} else {
-		stage(1, min(1, ntile - 1)); // (unconditional: the counted waits below stay exact)
-	}
+	stage_kv<D, false, KT>(Kb, kc, 0, kv_rows, kv_dim, g, wave, lane);
+	stage_kv<D, true, KT>(Vb, vc, 0, kv_rows, kv_dim, g, wave, lane);
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	__syncthreads();
 	int cur = 0;
 	for (int kt = 0; kt < ntile; ++kt) {
 		const int key0 = kt * KT;
-		if constexpr (NST == 2) {
-			if (kt + 1 < ntile) // next tile's LDS-DMA overlaps this tile's math
-				stage(cur ^ 1, kt + 1);
-		} else {
-			if (kt > 0)
-				__syncthreads(); // every wave is done with tile kt - 1: its stage is free
-			cur = kt % 3;
-			stage((kt + 2) % 3, min(kt + 2, ntile - 1));
-			asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory"); // tile kt landed (this wave's part)
-			__syncthreads();
+		if (kt + 1 < ntile) { // next tile's LDS-DMA overlaps this tile's math
+			stage_kv<D, false, KT>(Kb + (cur ^ 1) * KT * D, kc, key0 + KT, kv_rows, kv_dim, g, wave, lane);
+			stage_kv<D, true, KT>(Vb + (cur ^ 1) * KT * D, vc, key0 + KT, kv_rows, kv_dim, g, wave, lane);
 		}
 		const uint16_t *Ks = Kb + cur * KT * D;
 		const uint16_t *Vs = Vb + cur * KT * D;
@@ -275,14 +256,10 @@ __global__ __launch_bounds__(THREADS) void attn_prefill_kernel(const uint16_t *_
 					}
 				}
 		}
-		if constexpr (NST == 2) {
-			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-			__syncthreads(); // next tile landed; this tile's K / V reads are done
-			cur ^= 1;
-		}
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		__syncthreads(); // next tile landed; this tile's K / V reads are done
+		cur ^= 1;
 	}
-	if constexpr (NST == 3)
-		asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the clamped tail stages
 	// ---- normalise and store O[query][h * D + d] (f16, the Wo GEMM's A operand); d = 32 jd + crow(r)
 	if (qrow < T) {
 		const float inv = 1.0f / l;

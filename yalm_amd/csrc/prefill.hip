@@ -45,8 +45,6 @@ PfForms pf_forms_from_env() {
 		f.qkv1 = atoi(e) != 0;
 	if (const char *e = getenv("YALM_PF_SKL"))
 		f.skl = atoi(e) != 0;
-	if (const char *e = getenv("YALM_PF_AKT"))
-		f.akt = atoi(e) == 32 || atoi(e) == 33 ? atoi(e) : 64;
 	return f;
 }
 
@@ -241,38 +239,23 @@ pf::BSrc one(const void *w, int rows) {
 	return b;
 }
 
-template <int D, int KT, int NST = 2>
-int launch_attn_prefill_t(const dim3 &grid, const uint16_t *Q, const uint16_t *kc, const uint16_t *vc, int T,
-                          int pos0, int n_heads, int n_kv, uint16_t *O, hipStream_t st) {
-	static bool attr = false;
-	if (!attr) {
-		HIPCHK(hipFuncSetAttribute((const void *)pf::attn_prefill_kernel<D, KT, NST>,
-		                           hipFuncAttributeMaxDynamicSharedMemorySize,
-		                           (int)pf::attn_prefill_lds<D, KT, NST>()));
-		attr = true;
-	}
-	pf::attn_prefill_kernel<D, KT, NST><<<grid, pf::THREADS, pf::attn_prefill_lds<D, KT, NST>(), st>>>(
-	    Q, kc, vc, T, pos0, n_heads, n_kv, O);
-	return YALM_OK;
-}
-
-// kt: keys per tile (64, or 32: half the LDS and 158 instead of 175 VGPRs at head_dim 128,
-// three workgroups per CU instead of two; 33: 32-key tiles in 3 stages)
 int launch_attn_prefill(const uint16_t *Q, const uint16_t *kc, const uint16_t *vc, int T, int pos0, int n_heads,
-                        int n_kv, int head_dim, uint16_t *O, hipStream_t st, int kt) {
+                        int n_kv, int head_dim, uint16_t *O, hipStream_t st) {
 	const dim3 grid(n_heads, (T + pf::AQ - 1) / pf::AQ); // heads fastest: longest-first dispatch
-	if (head_dim == 128 && kt == 33)
-		TRY((launch_attn_prefill_t<128, 32, 3>(grid, Q, kc, vc, T, pos0, n_heads, n_kv, O, st)));
-	else if (head_dim == 128 && kt == 32)
-		TRY((launch_attn_prefill_t<128, 32>(grid, Q, kc, vc, T, pos0, n_heads, n_kv, O, st)));
-	else if (head_dim == 128)
-		TRY((launch_attn_prefill_t<128, 64>(grid, Q, kc, vc, T, pos0, n_heads, n_kv, O, st)));
-	else if (head_dim == 64 && kt == 33)
-		TRY((launch_attn_prefill_t<64, 32, 3>(grid, Q, kc, vc, T, pos0, n_heads, n_kv, O, st)));
-	else if (head_dim == 64 && kt == 32)
-		TRY((launch_attn_prefill_t<64, 32>(grid, Q, kc, vc, T, pos0, n_heads, n_kv, O, st)));
+	static bool attr_set = false;
+	if (!attr_set) {
+		HIPCHK(hipFuncSetAttribute((const void *)pf::attn_prefill_kernel<128>,
+		                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)pf::attn_prefill_lds<128>()));
+		HIPCHK(hipFuncSetAttribute((const void *)pf::attn_prefill_kernel<64>,
+		                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)pf::attn_prefill_lds<64>()));
+		attr_set = true;
+	}
+	if (head_dim == 128)
+		pf::attn_prefill_kernel<128><<<grid, pf::THREADS, pf::attn_prefill_lds<128>(), st>>>(Q, kc, vc, T, pos0,
+		                                                                                       n_heads, n_kv, O);
 	else if (head_dim == 64)
-		TRY((launch_attn_prefill_t<64, 64>(grid, Q, kc, vc, T, pos0, n_heads, n_kv, O, st)));
+		pf::attn_prefill_kernel<64><<<grid, pf::THREADS, pf::attn_prefill_lds<64>(), st>>>(Q, kc, vc, T, pos0,
+		                                                                                     n_heads, n_kv, O);
 	else {
 		set_err("prefill attention: head_dim must be 64 or 128");
 		return YALM_ERR_UNSUPPORTED;
@@ -424,7 +407,7 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 			}
 		}
 		TRY(launch_attn_prefill(b.Q, w.key_cache, w.value_cache, T, pos0, c.n_heads, c.n_kv_heads, c.head_dim, b.O,
-		                        st, f.akt));
+		                        st));
 		{
 			pf::E16Residual e;
 			e.x = b.X;
@@ -590,7 +573,7 @@ extern "C" int yalm_attn_prefill(uint16_t *o, const uint16_t *q, const uint16_t 
 	TRY(hd(dv, vc, kv * 2));
 	TRY(hd(dout, nullptr, T * q_dim * 2));
 	TRY(launch_attn_prefill((const uint16_t *)dq.p, (const uint16_t *)dk.p, (const uint16_t *)dv.p, T, pos0, n_heads,
-	                        n_kv_heads, head_dim, (uint16_t *)dout.p, nullptr, pf_forms_from_env().akt));
+	                        n_kv_heads, head_dim, (uint16_t *)dout.p, nullptr));
 	HIPCHK(hipDeviceSynchronize());
 	HIPCHK(hipMemcpy(o, dout.p, T * q_dim * 2, hipMemcpyDeviceToHost));
 	return YALM_OK;
