@@ -169,6 +169,12 @@ const char *yalm_kernel_name(yalm_decoder d, int kernel_id);
  * YALM_ATTN_WO not 0 at creation. 0 = two separate launches. The split-KV
  * attention output is handed to the Wo workgroups as {value, epoch} granules. */
 int yalm_decoder_attn_wo(yalm_decoder d);
+/* The fused launch's plan for a (per-rank) config when `slots` workgroups of 256
+ * threads are co-resident (occupancy x CUs): returns 1 and the key splits per kv head
+ * and the grid size, or 0 = separate attention and Wo launches (unsupported shape, or
+ * fewer than 2 key splits fit beside the mergers and Wo workgroups while contexts can
+ * exceed head mode). Pure host arithmetic: no device is touched. */
+int yalm_attn_wo_plan(const yalm_config *config, int slots, int *splits, int *grid);
 /* Timeline of the most recent fused attention + Wo launch (decoder created with
  * YALM_ATTN_WO_TRACE=1): 16 stamps per workgroup at [w * 16 + k]: k < 8
  * s_memrealtime (100 MHz), k + 8 the shader clock (s_memtime) at the same point; k = 0 start, 1 hand-off signalled (attention; 0 if this workgroup did not
@@ -233,6 +239,14 @@ int yalm_prefill(yalm_decoder d, const int *tokens, int n, int pos0, float *logp
 /* Average device time (ms) of one n-position prefill with log-probs (synthetic
  * token ids), over `iters` back-to-back runs (bench_prefill.py). */
 int yalm_prefill_time(yalm_decoder d, int n, int iters, float *avg_ms);
+/* Test / ablation hook: the prefill GEMM forms of decoder d (d = NULL: of the
+ * yalm_gemm_f16 test hook). spec = comma-separated key:value pairs, NULL or "" = the
+ * defaults: qkv|wo|glu|w2|cls|test:<128|192|256|320> force that GEMM's tile width;
+ * 8p:0 the 2-phase kernel; persist:0 one workgroup per tile; skinny:0 the large tiles
+ * for T <= 64 too; qkv1:0 the q and k|v GEMMs as two launches; skl:0 the skinny GEMMs'
+ * weights as register loads. Every form is exact against the others (tests). An
+ * unknown key is YALM_ERR_ARG. */
+int yalm_set_prefill_forms(yalm_decoder d, const char *spec);
 
 /* ---------------- test API: replaces infer.cu:890-1019 (model.h:370-384) ---------------- */
 /* Host pointers in and out; synchronous. dtype selects the weight type

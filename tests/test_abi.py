@@ -62,3 +62,37 @@ def test_runtime_raises_without_library(tmp_path, monkeypatch):
         assert "no cpu fallback" in str(e).lower()
     else:
         raise AssertionError("runtime imported without libyalm_hip.so")
+
+
+def test_attn_wo_plan_host_arithmetic():
+    """yalm_attn_wo_plan (pure host arithmetic, no device): Mistral-7B at 512 co-resident
+    slots (2 per CU x 256) fuses with the key splits that fit beside the mergers and the
+    Wo workgroups; a dim-8192 model (512 Wo workgroups) leaves fewer than 2
+    splits, so it keeps the separate launches instead of running every context in head
+    mode; shapes outside the fused contract (head_dim 64, Wo rows of 2 KB) never fuse."""
+    from yalm_amd import models as M
+    from yalm_amd import runtime
+
+    ok, S, grid = runtime.attn_wo_plan(M.MISTRAL_7B, 512)
+    assert ok and S == 25 and grid == 8 * (S + 3) + 32 + 256
+    big = M.MISTRAL_7B.with_(dim=8192)
+    assert runtime.attn_wo_plan(big, 512)[0] is False
+    # short windows (all contexts in head mode) may fuse with S = 1
+    ok, S, _ = runtime.attn_wo_plan(big.with_(max_seq_len=256), 512)
+    assert ok and S == 1
+    assert runtime.attn_wo_plan(M.MISTRAL_7B.with_(head_dim=64, n_heads=64, n_kv_heads=16), 512)[0] is False
+    assert runtime.attn_wo_plan(M.MISTRAL_7B.with_(n_heads=8, n_kv_heads=2), 512)[0] is False
+
+
+def test_prefill_forms_spec_validation():
+    """yalm_set_prefill_forms: explicit forms, no environment; a bad key / width is an
+    argument error (no device is touched for the NULL-decoder test-hook forms)."""
+    import pytest
+    from yalm_amd import runtime
+
+    runtime.set_gemm_forms("qkv:256,wo:192,8p:0,persist:0,skinny:0,qkv1:0,skl:0")
+    runtime.set_gemm_forms("")
+    for bad in ("bogus:1", "qkv:100", "qkv", "8p=0"):
+        with pytest.raises(runtime.YalmError):
+            runtime.set_gemm_forms(bad)
+    runtime.set_gemm_forms("")

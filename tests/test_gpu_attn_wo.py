@@ -120,9 +120,11 @@ def test_attn_wo_matches_separate_launches(name, cfg):
 
 
 def test_attn_wo_long_context_split_attention():
-    """kv_len up to 1040 (17 key chunks per kv head: at 32 splits one chunk per
-    workgroup, merged by the highest one): greedy tokens equal the oracle's the
-    whole way, then past max_seq_len."""
+    """kv_len up to 1040 (17 key chunks per kv head: one chunk per key split, a
+    partial per (head, split) folded by that query head's merger workgroup; the
+    last chunk is partial, 1040 = 16 x 64 + 16, so its rows past max_seq_len read
+    as zeros through the per-chunk descriptor): greedy tokens equal the oracle's
+    the whole way, then past max_seq_len."""
     cfg = BASE.with_(n_layers=2, max_seq_len=1040)
     t, dm, dec = make(cfg, seed=9)
     om = O.OracleModel(cfg, t)

@@ -39,39 +39,42 @@ def test_gemm_exact_integers(M_, N, K):
     np.testing.assert_array_equal(c, ref.astype(np.float32))
 
 
-# GEMM forms (yalm_amd/csrc/prefill_gemm.h), read when the decoder is created (the
-# yalm_gemm_f16 test hook: per call): "g16-256" / "g16-192" / "g16-128" / "g16-320" force
-# the 256-row tile's width on every GEMM it divides (256 / 192 / 128 run the 8-phase
-# gemm8p_kernel, "-2ph" the 2-phase gemm16_kernel, 320 is always 2-phase); "nopersist":
-# one workgroup per tile instead of the persistent tile loop. The round-2 128 x 128
-# kernel and its stage / wide forms were removed in round 4.
+# GEMM forms (yalm_amd/csrc/prefill_gemm.h), chosen explicitly through
+# yalm_set_prefill_forms (a decoder's, or with no decoder the yalm_gemm_f16 test hook's):
+# "g16-256" / "g16-192" / "g16-128" / "g16-320" force the 256-row tile's width on every
+# GEMM it divides (256 / 192 / 128 run the 8-phase gemm8p_kernel, "-2ph" the 2-phase
+# gemm16_kernel, 320 is always 2-phase); "nopersist": one workgroup per tile instead of
+# the persistent tile loop. The round-2 128 x 128 kernel and its stage / wide forms were
+# removed in round 4.
 G16_ALL = "qkv:{0},wo:{0},glu:{0},w2:{0},cls:{0},test:{0}"
-FORMS = {"auto": {}, "auto-qkv2": {"YALM_PF_QKV1": "0"},
-         "g16-256": {"YALM_PF_G16": G16_ALL.format(256)},
-         "g16-256-2ph": {"YALM_PF_G16": G16_ALL.format(256), "YALM_PF_8P": "0"}, "g16-128": {"YALM_PF_G16": G16_ALL.format(128)},
-         "g16-192": {"YALM_PF_G16": G16_ALL.format(192)},
-         "g16-192-2ph": {"YALM_PF_G16": G16_ALL.format(192), "YALM_PF_8P": "0"},
-         "g16-128-2ph": {"YALM_PF_G16": G16_ALL.format(128), "YALM_PF_8P": "0"},
-         "g16-256-nopersist": {"YALM_PF_G16": G16_ALL.format(256), "YALM_PF_PERSIST": "0"},
-         "g16-320": {"YALM_PF_G16": G16_ALL.format(320)}}
+FORMS = {"auto": "", "auto-qkv2": "qkv1:0",
+         "g16-256": G16_ALL.format(256),
+         "g16-256-2ph": G16_ALL.format(256) + ",8p:0", "g16-128": G16_ALL.format(128),
+         "g16-192": G16_ALL.format(192),
+         "g16-192-2ph": G16_ALL.format(192) + ",8p:0",
+         "g16-128-2ph": G16_ALL.format(128) + ",8p:0",
+         "g16-256-nopersist": G16_ALL.format(256) + ",persist:0",
+         "g16-320": G16_ALL.format(320)}
 
 
 @pytest.mark.parametrize("form", list(FORMS))
 @pytest.mark.parametrize("M_,N,K", [(200, 256, 192), (37, 768, 128), (1, 256, 64), (513, 5120, 640), (300, 384, 64),
                                     (513, 512, 320), (260, 768, 448), (256, 256, 576), (70, 512, 128),
                                     (1100, 16384, 192)])
-def test_gemm_forms_exact(form, M_, N, K, monkeypatch):
+def test_gemm_forms_exact(form, M_, N, K):
     """Every tile form is exact on f16-exact integer data (any
     staging race or fragment-map error shows as a wrong integer); K tiles 1..10
     (odd and even counts: the 8-phase kernel's iteration covers two K tiles);
     1100 x 16384: more 256 x 256 tiles (320) than CUs, so the persistent tile loop runs."""
-    for k, v in FORMS[form].items():
-        monkeypatch.setenv(k, v)
     rng = np.random.default_rng(M_ + N + K)
     a = rng.integers(-4, 5, size=(M_, K)).astype(np.float16)
     w = rng.integers(-4, 5, size=(N, K)).astype(np.float16)
     w[:, 0] += np.arange(N, dtype=np.float16) % 7
-    c = rt().gemm_f16(a, w)
+    rt().set_gemm_forms(FORMS[form])
+    try:
+        c = rt().gemm_f16(a, w)
+    finally:
+        rt().set_gemm_forms("")
     ref = a.astype(np.float64) @ w.astype(np.float64).T  # exact: small integers
     np.testing.assert_array_equal(c, ref.astype(np.float32))
 
@@ -140,17 +143,16 @@ CFGS = {
 @pytest.mark.parametrize("cfg_name", ["gqa-d128", "d768"])
 @pytest.mark.parametrize("form", ["auto", "auto-qkv2", "g16-256", "g16-256-2ph", "g16-128", "g16-128-2ph", "g16-192",
                                   "g16-192-2ph", "g16-320", "g16-256-nopersist"])
-def test_prefill_forms_match_decode(form, cfg_name, monkeypatch):
+def test_prefill_forms_match_decode(form, cfg_name):
     """The whole prefill in each GEMM form (incl. the vocab-tiled logits epilogue, the
     one-launch two-depth QKV GEMM ("auto") and the k | v launch at a column offset over
     the [hi | lo] operand ("auto-qkv2", forced widths))."""
-    for k, v in FORMS[form].items():
-        monkeypatch.setenv(k, v)
     cfg = CFGS[cfg_name]
     R = rt()
     dm = R.DeviceModel.synthetic(cfg, seed=4)
     tokens = np.random.default_rng(5).integers(0, cfg.vocab_size, size=90).astype(np.int32)
     dec_p = R.Decoder(dm)
+    dec_p.set_prefill_forms(FORMS[form])
     dec_d = R.Decoder(dm)
     try:
         err = np.max(np.abs(dec_p.prefill(tokens)[:89] - _decode_logprobs(dec_d, tokens)))
@@ -193,22 +195,20 @@ def test_prefill_matches_decode(name, n):
 
 @pytest.mark.parametrize("cfg_name", ["gqa-d128", "d768", "gelu-d128"])
 @pytest.mark.parametrize("n", [1, 5, 16, 17, 33, 64])
-def test_prefill_short_prompt_paths(cfg_name, n, monkeypatch):
+def test_prefill_short_prompt_paths(cfg_name, n):
     """Short prompts (T <= 64) run the split-K skinny GEMMs (prefill_skinny.h): their
     log p and the KV cache they leave (next decode step's logits) against the decode
-    engine and against the 256-row-tile path of the same prompt (YALM_PF_SKINNY=0);
+    engine and against the 256-row-tile path of the same prompt (form skinny:0);
     every M-tile count 1..4 and the row tails."""
     cfg = CFGS[cfg_name]
     R = rt()
     dm = R.DeviceModel.synthetic(cfg, seed=8)
     tokens = np.random.default_rng(100 + n).integers(0, cfg.vocab_size, size=n).astype(np.int32)
     dec_s = R.Decoder(dm)
-    monkeypatch.setenv("YALM_PF_SKINNY", "0")
     dec_l = R.Decoder(dm)
-    monkeypatch.delenv("YALM_PF_SKINNY")
-    monkeypatch.setenv("YALM_PF_SKL", "0")  # the skinny GEMMs' weights as register loads
+    dec_l.set_prefill_forms("skinny:0")
     dec_r = R.Decoder(dm)
-    monkeypatch.delenv("YALM_PF_SKL")
+    dec_r.set_prefill_forms("skl:0")  # the skinny GEMMs' weights as register loads
     dec_d = R.Decoder(dm)
     try:
         lp_s, lp_l, lp_r = dec_s.prefill(tokens), dec_l.prefill(tokens), dec_r.prefill(tokens)

@@ -59,19 +59,26 @@ constexpr int attn_nk() {
 }
 
 // One lane's K / V rows of a 64-key chunk through buffer resources: the per-lane byte
-// offsets (row group, piece) are fixed, the chunk is a wave-uniform soffset. Rows past
-// max_seq_len (the descriptor's end) read as zeros and move no data, so a prefetch past
-// the last chunk passes soffset = end and costs nothing. Round 4 first used flat loads
-// at per-chunk 64-bit addresses: their address temporaries re-used the registers of
-// the previous chunk's loads, and hipcc drained vmcnt to 0 at every chunk-loop
-// iteration -- the next chunk's loads waited for the prefetch (one load latency per
-// two chunks).
+// offsets (row group, piece) are fixed voffsets; each chunk gets its OWN descriptor pair,
+// built in SGPRs: base = the cache + t0 rows, num_records = the chunk's rows inside the
+// cache (0 when the chunk is not live), so a dead load moves no data and the rows of a
+// partial final chunk past max_seq_len read as zeros through voffset alone. Round 4 put
+// the chunk in soffset of one whole-cache descriptor and relied on the range check
+// covering soffset; tools/soffset_probe.hip shows gfx950 does check voffset + soffset
+// (profiles/r5_soffset_probe.txt: soffset = num_records reads zero), so that form read
+// nothing past the allocation either -- but its num_records (max_seq_len x row bytes)
+// wrapped at 4 GiB, and the per-chunk descriptor needs neither the
+// undocumented rule nor 32-bit cache sizes: num_records covers at most 64 rows.
+// Round 4 first used flat loads at per-chunk 64-bit addresses: their address temporaries
+// re-used the registers of the previous chunk's loads, and hipcc drained vmcnt to 0 at
+// every chunk-loop iteration -- the next chunk's loads waited for the prefetch (one load
+// latency per two chunks). The descriptors are scalar, so that does not come back.
 template <int D>
 struct KvRows {
 	static constexpr int LPK = D / 8, KPW = 64 / LPK, RSTEP = (ATTN_THREADS / 64) * KPW;
 	static constexpr int NK = attn_nk<D>();
-	__amdgpu_buffer_rsrc_t kr, vr;
-	uint32_t rowb, end;
+	const char *kb, *vb;
+	uint32_t rowb, msl; // bytes per cache row, rows per layer (max_seq_len)
 	uint32_t voff[NK];
 	__device__ __forceinline__ KvRows(const uint16_t *kc, const uint16_t *vc, int n_kv_heads, int max_seq_len, int g) {
 		const int lane = threadIdx.x & 63;
@@ -82,12 +89,12 @@ struct KvRows {
 			const uint64_t a = (uint64_t)p;
 			const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
 			const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-			return (void *)(((uint64_t)hi << 32) | lo);
+			return (const char *)(((uint64_t)hi << 32) | lo);
 		};
 		rowb = (uint32_t)__builtin_amdgcn_readfirstlane(n_kv_heads * D * 2);
-		end = (uint32_t)__builtin_amdgcn_readfirstlane((int)((uint32_t)max_seq_len * rowb));
-		kr = __builtin_amdgcn_make_buffer_rsrc(uni(kc), (short)0, (int)end, 0x00020000);
-		vr = __builtin_amdgcn_make_buffer_rsrc(uni(vc), (short)0, (int)end, 0x00020000);
+		msl = (uint32_t)__builtin_amdgcn_readfirstlane(max_seq_len);
+		kb = uni(kc);
+		vb = uni(vc);
 #pragma unroll
 		for (int i = 0; i < NK; ++i)
 			voff[i] = (uint32_t)(tl0 + i * RSTEP) * rowb + (uint32_t)(g * D + piece * 8) * 2;
@@ -96,12 +103,22 @@ struct KvRows {
 	__device__ __forceinline__ void load(int t0, bool live, u32x4_t (&kw)[NK], u32x4_t (&vw)[NK]) const {
 		// wave-uniform (T20); t0 and live must come from scalar values (attn_core keeps its
 		// chunk loop in SGPRs): a VALU select here took a register of the previous chunk's
-		// loads and cost a vmcnt(0) per chunk
-		const uint32_t so = live ? (uint32_t)t0 * rowb : end;
+		// loads and cost a vmcnt(0) per chunk. Branch-free scalar arithmetic: a 64-bit compare
+		// here became scalar branches, and hipcc then drained vmcnt(0) at the join.
+		const uint32_t t = (uint32_t)t0;
+		// rows of the cache from t0 on, at most one chunk (a live chunk has t0 < kv_len <=
+		// max_seq_len). Only s_min / s_cselect: a clamp became v_med3 and an unsigned
+		// saturating subtract v_sub clamp -- VALU temporaries that re-used a register of the
+		// previous chunk's loads (a vmcnt(0) per chunk) or forced a waterfall loop
+		const int rows = min((int)msl - t0, attn_chunk<D>());
+		const int nrec = live ? rows * (int)rowb : 0;
+		const uint64_t o = (uint64_t)t * rowb;
+		const __amdgpu_buffer_rsrc_t kr = __builtin_amdgcn_make_buffer_rsrc((void *)(kb + o), (short)0, nrec, 0x00020000);
+		const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc((void *)(vb + o), (short)0, nrec, 0x00020000);
 #pragma unroll
 		for (int i = 0; i < NK; ++i) {
-			kw[i] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(kr, voff[i], so, 0));
-			vw[i] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(vr, voff[i], so, 0));
+			kw[i] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(kr, voff[i], 0, 0));
+			vw[i] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(vr, voff[i], 0, 0));
 		}
 	}
 };
@@ -249,7 +266,7 @@ __device__ __forceinline__ bool attn_core(int g, int hq0, int Gh, int c_first, i
                                           unsigned ptag, float *out, float *att_dbg, unsigned gtag,
                                           unsigned long long *ts, bool trace_on) {
 	constexpr int CHUNK = attn_chunk<D>();
-	// the chunk loop's values in SGPRs (KvRows::load's soffset is computed from them)
+	// the chunk loop's values in SGPRs (KvRows::load's descriptors are computed from them)
 	c_first = __builtin_amdgcn_readfirstlane(c_first);
 	cstride = __builtin_amdgcn_readfirstlane(cstride);
 	ns = __builtin_amdgcn_readfirstlane(ns);
@@ -266,7 +283,6 @@ __device__ __forceinline__ bool attn_core(int g, int hq0, int Gh, int c_first, i
 
 	const int G = n_heads / n_kv_heads;
 	const int hb = g * G + hq0; // first query head computed here
-	const int kv_dim = n_kv_heads * D;
 	const int lane = threadIdx.x & 63;
 	const int wave = threadIdx.x >> 6;
 	const int tid = threadIdx.x;
@@ -486,8 +502,9 @@ __device__ __forceinline__ bool attn_core(int g, int hq0, int Gh, int c_first, i
 
 	// chunks c_first, c_first + cstride, ...: straight-line loads for one chunk; beyond
 	// it the next chunk's rows are loaded before the current one is computed (the prefetch
-	// past the last chunk re-reads row kv_len - 1: unconditional loads keep hipcc's vmcnt
-	// counting exact, a conditional one would drain to 0 before every load)
+	// past the last chunk is issued with a zero-record descriptor and moves no data,
+	// KvRows: unconditional loads keep hipcc's vmcnt counting exact, a conditional one
+	// would drain to 0 before every load)
 	using T_ = std::true_type;
 	using F_ = std::false_type;
 	if (c_first + cstride >= ns) {
@@ -646,7 +663,7 @@ __device__ __forceinline__ bool attn_decode_body(int g, int u, int S, int head_m
 	// holds keys (their speculative loads were 6.3 MB of dead reads per layer at short
 	// contexts, 192 units x 32 KB: fused fp8 kv 17 8.3 -> 7.9 us, fp16 bench +0.9%, long
 	// context -0.2%, profiles/r4q_split_spec.txt). The instruction stays unconditional
-	// (a split unit's passes the descriptor's end and moves no data): hipcc's vmcnt
+	// (a split unit's gets a zero-record descriptor and moves no data): hipcc's vmcnt
 	// counting stays static.
 	u32x4_t kA[NK], vA[NK];
 	const KvRows<D> rows(kc, vc, n_kv_heads, max_seq_len, g);

@@ -80,9 +80,9 @@ struct PrefillBufs {
 };
 
 // Prefill GEMM forms (prefill.hip): per GEMM kind the large-tile width (-1 = auto,
-// 128 / 192 / 256 / 320), the 8-phase schedule, the persistent tile loop. Fixed at
-// decoder creation (YALM_PF_G16 / YALM_PF_8P / YALM_PF_PERSIST select other exact forms
-// for the tests); never re-read per launch.
+// 128 / 192 / 256 / 320), the 8-phase schedule, the persistent tile loop. The defaults at
+// decoder creation; other exact forms only through yalm_set_prefill_forms (the tests);
+// never read from the environment by the production library.
 struct PfForms {
 	int g16[6] = {-1, -1, -1, -1, -1, -1}; // qkv, wo, glu, w2, cls, test
 	bool p8 = true, persist = true;
@@ -90,7 +90,7 @@ struct PfForms {
 	bool qkv1 = true;       // the q and k | v GEMMs as ONE two-depth launch when BN 256 fits both
 	bool skl = true;        // skinny GEMMs: weight rows staged by LDS-DMA (prefill_skinny.h)
 };
-PfForms pf_forms_from_env();
+PfForms pf_forms_default(); // prefill.hip: the production forms (A/B build: YALM_PF_FORMS)
 
 // ------------------------------------------------------------------ decoder
 enum { GRAPH_HYDRATE = 0, GRAPH_LOGITS = 1, GRAPH_GREEDY = 2, N_GRAPHS = 3 };

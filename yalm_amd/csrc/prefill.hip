@@ -7,7 +7,9 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
+#include <string>
 #include <type_traits>
 #include <vector>
 
@@ -19,33 +21,72 @@
 // Large-tile GEMM form per GEMM kind (prefill_gemm.h): the tile width BN of the
 // 256-row tile. Default: auto -- the BN dividing N that minimises rounds x (BN + 64),
 // rounds = ceil(tiles / CUs): a 256-CU chip should get whole rounds of large tiles
-// (Llama-3B Wo / W2 N 3072 -> 192). YALM_PF_G16 = "qkv:256,wo:128,..." forces widths
-// (the exact-form tests), YALM_PF_8P=0 the 2-phase kernel, YALM_PF_PERSIST=0 one
-// workgroup per tile, YALM_PF_SKINNY=0 the large tiles at T <= 64 too (prefill_skinny.h
-// otherwise), YALM_PF_QKV1=0 the q and k | v GEMMs as two launches, YALM_PF_SKL=0 the
-// skinny GEMMs' weights as register loads instead of LDS-DMA stages. All of them are read once, at decoder creation (PfForms); the
-// kernel-level test hook yalm_gemm_f16 reads them per call.
-PfForms pf_forms_from_env() {
+// (Llama-3B Wo / W2 N 3072 -> 192). Other exact forms (the tests, ablations) are chosen
+// explicitly through yalm_set_prefill_forms: "qkv:256,wo:128,..." forces widths, 8p:0
+// the 2-phase kernel, persist:0 one workgroup per tile, skinny:0 the large tiles at
+// T <= 64 too (prefill_skinny.h otherwise), qkv1:0 the q and k | v GEMMs as two
+// launches, skl:0 the skinny GEMMs' weights as register loads instead of LDS-DMA stages.
+// The production library reads no environment for them; the A/B build (-DYALM_AB)
+// takes a decoder's initial forms from YALM_PF_FORMS (same syntax).
+static int parse_pf_forms(const char *spec, PfForms &f) {
 	static const char *names[6] = {"qkv", "wo", "glu", "w2", "cls", "test"};
-	PfForms f;
-	if (const char *e = getenv("YALM_PF_G16")) {
-		for (int k = 0; k < 6; ++k) {
-			const char *p = strstr(e, names[k]);
-			if (p && p[strlen(names[k])] == ':')
-				f.g16[k] = atoi(p + strlen(names[k]) + 1);
+	f = PfForms{};
+	if (!spec)
+		return YALM_OK;
+	const char *p = spec;
+	while (*p) {
+		char key[16];
+		int val = 0, n = 0;
+		if (sscanf(p, "%15[^:,]:%d%n", key, &val, &n) != 2) {
+			set_err(std::string("yalm_set_prefill_forms: bad spec at '") + p + "'");
+			return YALM_ERR_ARG;
 		}
+		bool known = false;
+		for (int k = 0; k < 6; ++k)
+			if (!strcmp(key, names[k])) {
+				ARGCHK(val == 128 || val == 192 || val == 256 || val == 320,
+				       "yalm_set_prefill_forms: a tile width is 128, 192, 256 or 320");
+				f.g16[k] = val;
+				known = true;
+			}
+		if (!strcmp(key, "8p"))
+			f.p8 = val != 0, known = true;
+		else if (!strcmp(key, "persist"))
+			f.persist = val != 0, known = true;
+		else if (!strcmp(key, "skinny"))
+			f.no_skinny = val == 0, known = true;
+		else if (!strcmp(key, "qkv1"))
+			f.qkv1 = val != 0, known = true;
+		else if (!strcmp(key, "skl"))
+			f.skl = val != 0, known = true;
+		if (!known) {
+			set_err(std::string("yalm_set_prefill_forms: unknown key '") + key + "'");
+			return YALM_ERR_ARG;
+		}
+		p += n;
+		if (*p == ',')
+			++p;
 	}
-	if (const char *e = getenv("YALM_PF_8P"))
-		f.p8 = atoi(e) != 0;
-	if (const char *e = getenv("YALM_PF_PERSIST"))
-		f.persist = atoi(e) != 0;
-	if (const char *e = getenv("YALM_PF_SKINNY"))
-		f.no_skinny = atoi(e) == 0;
-	if (const char *e = getenv("YALM_PF_QKV1"))
-		f.qkv1 = atoi(e) != 0;
-	if (const char *e = getenv("YALM_PF_SKL"))
-		f.skl = atoi(e) != 0;
+	return YALM_OK;
+}
+
+PfForms pf_forms_default() {
+	PfForms f;
+	if (parse_pf_forms(ab_env("YALM_PF_FORMS"), f) != YALM_OK)
+		f = PfForms{};
 	return f;
+}
+
+static PfForms g_test_forms; // the forms of the yalm_gemm_f16 test hook
+
+extern "C" int yalm_set_prefill_forms(yalm_decoder d, const char *spec) {
+	PfForms f;
+	TRY(parse_pf_forms(spec, f));
+	if (d)
+		d->pf_forms = f;
+	else
+		g_test_forms = f;
+	return YALM_OK;
 }
 
 namespace {
@@ -554,7 +595,7 @@ extern "C" int yalm_gemm_f16(float *c, const uint16_t *a, const uint16_t *w, int
 	e16.c = (float *)dc.p;
 	e16.ldc = N;
 	e16.M = M;
-	const PfForms f = pf_forms_from_env(); // a test hook: the forms of this call's environment
+	const PfForms f = g_test_forms; // a test hook: the forms set by yalm_set_prefill_forms(NULL, ...)
 	TRY(launch_plain(f, pick_bn(f, PG_TEST, M, N, false), (const uint16_t *)da.p, K, M, K, K, one(dw.p, N), N, e16,
 	                 nullptr));
 	HIPCHK(hipDeviceSynchronize());

@@ -356,7 +356,45 @@ static const void *attn_wo_pick(int dtype, int G, int XS) {
 		return XS == 1 ? attn_wo_fn_g<WF16, 1>(G) : attn_wo_fn_g<WF16, 2>(G);
 	return XS == 1 ? attn_wo_fn_g<WF8, 1>(G) : attn_wo_fn_g<WF8, 2>(G);
 }
-// Single-GPU decoders with head_dim 128, G <= 8 and fp16 / fp8 Wo rows of 4 or 8 KB.
+// The fused launch's plan for a (per-rank) config: 1 with the key splits S and the grid,
+// or 0 = separate attention and Wo launches. Fused needs head_dim 128, G <= 8, fp16 / fp8
+// Wo rows of 4 or 8 KB, and the whole grid (attention, one merger per query head, Wo)
+// within the co-resident workgroup slots: a workgroup past them is dispatched only when
+// an earlier one exits, and at short contexts every attention workgroup without keys
+// still holds its slot for the kv_len load (S 32 at Mistral: 256 + 32 + 256 = 544 > 512
+// slots put the last 32 Wo slices ~2 us late, fused launch 8.9 -> 11.2 us at kv 17). When
+// fewer than 2 key splits fit (dim 8192 has 512 Wo workgroups) the fused launch
+// would run every context in head mode -- one workgroup per query head over all the
+// chunks -- so the separate launches (standalone attention at ATTN_SPLITS) are kept.
+// Pure host arithmetic (tests/test_abi.py calls it without a GPU).
+extern "C" int yalm_attn_wo_plan(const yalm_config *cp, int slots, int *splits, int *grid) {
+	if (!cp || slots <= 0)
+		return 0;
+	const yalm_config &c = *cp;
+	if (c.head_dim != 128 || c.n_kv_heads <= 0 || c.n_heads % c.n_kv_heads)
+		return 0;
+	const int G = c.n_heads / c.n_kv_heads;
+	if (G < 1 || G > 8 || (c.weight_dtype != YALM_F16 && c.weight_dtype != YALM_F8E5M2))
+		return 0;
+	const int rb = c.n_heads * c.head_dim * (c.weight_dtype == YALM_F16 ? 2 : 1);
+	if ((rb != 4096 && rb != 8192) || c.dim < AWO_RPW)
+		return 0;
+	const int nchunks = (c.max_seq_len + attn_chunk<128>() - 1) / attn_chunk<128>();
+	const int n_wo = (c.dim + AWO_RPW - 1) / AWO_RPW;
+	const int fit = (slots - c.n_heads - n_wo) / c.n_kv_heads - (G - 1); // key splits: S + G - 1 units per kv head
+	const char *senv = ab_env("YALM_AWO_SPLITS");
+	const int S = std::max(1, std::min(nchunks, senv ? std::max(1, std::min(ATTN_MAX_SPLITS, atoi(senv)))
+	                                                 : std::min(ATTN_SPLITS, fit)));
+	if (!senv && fit < 2 && nchunks > ATTN_HEAD_MAX)
+		return 0;
+	if (splits)
+		*splits = S;
+	if (grid)
+		*grid = c.n_kv_heads * (S + G - 1) + c.n_heads + n_wo;
+	return 1;
+}
+
+// Single-GPU decoders whose plan (yalm_attn_wo_plan) fuses.
 static int attn_wo_init(yalm_decoder_s *d) {
 	const yalm_config &c = d->c;
 	const char *env = getenv("YALM_ATTN_WO");
@@ -365,36 +403,20 @@ static int attn_wo_init(yalm_decoder_s *d) {
 	if (d->comm || d->ipc || d->tp_size > 1 || c.head_dim != 128)
 		return YALM_OK;
 	const int G = c.n_heads / c.n_kv_heads;
-	if (G < 1 || G > 8 || (c.weight_dtype != YALM_F16 && c.weight_dtype != YALM_F8E5M2))
-		return YALM_OK;
 	const int rb = c.n_heads * c.head_dim * (c.weight_dtype == YALM_F16 ? 2 : 1);
-	if (rb != 4096 && rb != 8192)
-		return YALM_OK;
-	if (c.dim < AWO_RPW)
+	if (!yalm_attn_wo_plan(&c, 1 << 30, nullptr, nullptr))
 		return YALM_OK;
 	int occ = 0; // the Wo workgroups spin, but only on attention workgroups dispatched before them
 	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, attn_wo_pick(c.weight_dtype, G, rb / 4096), ATTN_THREADS,
 	                                                 0) != hipSuccess ||
 	    occ < 1)
 		return YALM_OK;
-	const int nchunks = (c.max_seq_len + attn_chunk<128>() - 1) / attn_chunk<128>();
+	if (!yalm_attn_wo_plan(&c, occ * device_cu_count(), &d->awo_S, &d->awo_nb))
+		return YALM_OK;
 	// per layer: the attention output as {value, epoch} granules (zero tags never match:
 	// the epoch is >= 1 from the first forward / yalm_block on)
 	const size_t gran = (size_t)c.n_layers * c.n_heads * c.head_dim;
 	TRY(dalloc(d, (void **)&d->awo_gran, sizeof(unsigned long long) * gran));
-	// key-chunk splits per kv head: as the standalone attention launch, but the whole grid
-	// (attention, one merger per query head, Wo) must fit the co-resident workgroup slots:
-	// a workgroup past them is dispatched only when an earlier one exits, and at short
-	// contexts every attention workgroup without keys still holds its slot for the
-	// kv_len load (S 32 at Mistral: 256 + 32 + 256 = 544 > 512 slots put the last 32 Wo
-	// slices ~2 us late, fused launch 8.9 -> 11.2 us at kv 17)
-	const int n_wo = (c.dim + AWO_RPW - 1) / AWO_RPW;
-	const int slots = occ * device_cu_count();
-	const int fit = (slots - c.n_heads - n_wo) / c.n_kv_heads - (G - 1); // key splits: S + G - 1 units per kv head
-	const char *senv = ab_env("YALM_AWO_SPLITS");
-	d->awo_S = std::max(1, std::min(nchunks, senv ? std::max(1, std::min(ATTN_MAX_SPLITS, atoi(senv)))
-	                                                : std::min(ATTN_SPLITS, fit)));
-	d->awo_nb = c.n_kv_heads * (d->awo_S + G - 1) + c.n_heads + n_wo;
 	const char *denv = ab_env("YALM_ATTN_WO_DELAY");
 	// default 0.2 us (fp16) / 0.5 us (fp8): the attention workgroups' K/V loads reach HBM
 	// ahead of the Wo stream. fp16 (33.5 MB, slice lands ~5.4 us, after the heads):
@@ -832,7 +854,7 @@ static int create_decoder(const yalm_config *config, const yalm_model_weights *w
 	const int q_dim = c.n_heads * c.head_dim, kv_dim = c.n_kv_heads * c.head_dim;
 	const int nsplit = attn_nsplit(c.max_seq_len);
 	d->tokens_cap = 1 << 16;
-	d->pf_forms = pf_forms_from_env();
+	d->pf_forms = pf_forms_default();
 	d->eager = getenv("YALM_EAGER") && atoi(getenv("YALM_EAGER")) != 0;
 	d->graph_sync = getenv("YALM_GRAPH_SYNC") && atoi(getenv("YALM_GRAPH_SYNC")) != 0;
 	// geometry overrides for A/B runs without a rebuild (same meaning as yalm_set_gemv_config):

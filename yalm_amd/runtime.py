@@ -124,6 +124,8 @@ _sig("yalm_copy_2d", c_int, [c_void_p, ctypes.c_size_t, c_void_p, ctypes.c_size_
 _sig("yalm_prefill_time", c_int, [c_void_p, c_int, c_int, ctypes.POINTER(c_float)])
 _sig("yalm_gemm_f16", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int])
 _sig("yalm_attn_prefill", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int])
+_sig("yalm_set_prefill_forms", c_int, [c_void_p, ctypes.c_char_p])
+_sig("yalm_attn_wo_plan", c_int, [c_void_p, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)])
 
 EXPORTED = [
     "yalm_last_error", "yalm_set_device", "yalm_upload", "yalm_alloc", "yalm_download", "yalm_register_host",
@@ -134,7 +136,7 @@ EXPORTED = [
     "yalm_prefill", "yalm_prefill_time", "yalm_gemm_f16", "yalm_attn_prefill", "yalm_tp_unique_id",
     "yalm_decoder_create_tp", "yalm_copy_2d", "yalm_tp_ipc_alloc", "yalm_decoder_create_tp_ipc",
     "yalm_decoder_attn_wo", "yalm_attn_wo_trace", "yalm_stream_envelope",
-    "yalm_argmax",
+    "yalm_argmax", "yalm_set_prefill_forms", "yalm_attn_wo_plan",
 ]
 
 HYDRATE_KV_CACHE, OUTPUT_LOGITS = 0, 1
@@ -218,6 +220,20 @@ def gemm_f16(a: np.ndarray, w: np.ndarray) -> np.ndarray:
     c = np.zeros((M, N), np.float32)
     check(lib.yalm_gemm_f16(_ptr(c), _ptr(a), _ptr(w), M, N, K))
     return c
+
+
+def set_gemm_forms(spec: str = "") -> None:
+    """The prefill GEMM forms of the gemm_f16 test hook (yalm_set_prefill_forms(NULL, spec))."""
+    check(lib.yalm_set_prefill_forms(None, spec.encode() if spec else None))
+
+
+def attn_wo_plan(cfg: M.ModelConfig, slots: int):
+    """(fused?, key splits, grid) of the fused attention + Wo launch for cfg at `slots`
+    co-resident workgroups (yalm_attn_wo_plan: host arithmetic, no device)."""
+    c = Config.from_model(cfg)
+    s, g = c_int(), c_int()
+    ok = lib.yalm_attn_wo_plan(ctypes.byref(c), slots, ctypes.byref(s), ctypes.byref(g))
+    return bool(ok), s.value, g.value
 
 
 def attn_prefill(q, kc, vc, T, pos0, n_heads, n_kv_heads, head_dim) -> np.ndarray:
@@ -404,6 +420,10 @@ class Decoder:
         out = np.zeros(len(tok), np.float32) if logprobs else None
         check(lib.yalm_prefill(self.h, _ptr(tok), len(tok), pos0, _ptr(out) if logprobs else None))
         return out
+
+    def set_prefill_forms(self, spec: str = "") -> None:
+        """Select another exact prefill GEMM form (yalm_set_prefill_forms), "" = defaults."""
+        check(lib.yalm_set_prefill_forms(self.h, spec.encode() if spec else None))
 
     def prefill_time(self, n: int, iters: int = 3) -> float:
         ms = c_float()
