@@ -148,6 +148,10 @@ static void softmax(float *o, const float *x, int size) {
 	}
 }
 
+void orc_softmax(float *o, const float *x, int size) {
+	softmax(o, x, size);
+}
+
 /* infer.cpp:187-197 */
 static inline float gelu(float x) {
 	return 0.5f * x * (1.0f + tanhf(0.797885f * (x + 0.044715f * x * x * x)));

@@ -72,6 +72,7 @@ void orc_matmul_f16(float *xout, const float *x, const uint16_t *w, int n, int d
 void orc_matmul_f8(float *xout, const float *x, const uint8_t *w, int n, int d);
 void orc_rmsnorm(float *o, const float *x, const float *w, int size, float eps);        /* infer.cpp:134-144 */
 void orc_rope(float *vec, int d, int head_dim, int pos, float theta, int rotary_dim);    /* infer.cpp:200-213 */
+void orc_softmax(float *o, const float *x, int size);                                    /* infer.cpp:170-185 */
 void orc_attn(float *xout, float *atth, const float *qh, const uint16_t *kh, const uint16_t *vh, int head_dim,
               int n_kv_heads, int kv_len);                                                 /* infer.cpp:216-248 */
 void orc_mha(float *xout, float *att, const uint16_t *kb, const uint16_t *vb, const float *q, int head_dim, int kv_len,

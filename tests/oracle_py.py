@@ -62,6 +62,7 @@ _s("orc_matmul_f16", None, [vp, vp, vp, ci, ci])
 _s("orc_matmul_f8", None, [vp, vp, vp, ci, ci])
 _s("orc_rmsnorm", None, [vp, vp, vp, ci, cf])
 _s("orc_rope", None, [vp, ci, ci, ci, cf, ci])
+_s("orc_softmax", None, [vp, vp, ci])
 _s("orc_attn", None, [vp, vp, vp, vp, vp, ci, ci, ci])
 _s("orc_mha", None, [vp, vp, vp, vp, vp, ci, ci, ci, ci, ci])
 _s("orc_ffn", None, [vp, vp, vp, vp, vp, ci, ci, ci, ci])

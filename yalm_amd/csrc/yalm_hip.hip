@@ -882,11 +882,16 @@ static int create_decoder(const yalm_config *config, const yalm_model_weights *w
 	    (r = dalloc(d, (void **)&d->inv_freq, sizeof(float) * c.head_dim / 2)) ||
 	    (r = dalloc(d, (void **)&d->tokens, sizeof(int) * d->tokens_cap)))
 		return fail(r);
-	// RoPE frequencies on the host with the CPU oracle's expression
-	// (infer.cpp:203): 1/powf(theta, j/rotary_dim) for even j < rotary_dim, else 0.
+	// RoPE frequencies on the host, bit for bit as the reference's compiled rope computes
+	// them. infer.cpp:203 reads 1/powf(theta, j/rotary_dim), but under its -ffast-math
+	// (Makefile:36-39) gcc emits r = 1.0f / rotary_dim; powf(theta, -(j * r)) (one scalar
+	// glibc powf call; the division folded into the exponent): a freq one ulp away moves
+	// the angle pos * freq by pos ulps, 2e-4 rad at pos 4095 -- tests/test_gpu_ref_glue.py
+	// measured 60 f16 ulps on a K row against the reference's own rope before this form.
 	std::vector<float> inv(c.head_dim / 2);
+	const float rinv = 1.0f / (float)c.rotary_dim;
 	for (int j = 0; j < c.head_dim; j += 2)
-		inv[j / 2] = j >= c.rotary_dim ? 0.f : 1.0f / powf(c.rope_theta, (float)j / (float)c.rotary_dim);
+		inv[j / 2] = j >= c.rotary_dim ? 0.f : powf(c.rope_theta, -((float)j * rinv));
 	if (hipMemcpy(d->inv_freq, inv.data(), sizeof(float) * inv.size(), hipMemcpyHostToDevice) != hipSuccess) {
 		set_err("inv_freq upload failed");
 		return fail(YALM_ERR_HIP);

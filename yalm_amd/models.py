@@ -285,9 +285,12 @@ def e5m2_to_f32(b: np.ndarray) -> np.ndarray:
 
 
 def rope_inv_freq(c: ModelConfig) -> np.ndarray:
-    j = np.arange(0, c.head_dim, 2)
-    with np.errstate(divide="ignore"):
-        f = 1.0 / np.power(np.float32(c.rope_theta), (j / c.rotary_dim).astype(np.float32))
+    """The reference's compiled RoPE frequencies (infer.cpp:203 under -ffast-math:
+    powf(theta, -(j * (1 / rotary_dim))), the form the decoder uploads); numpy's float32
+    power stands in for glibc powf (may differ by an ulp: analysis tools only)."""
+    j = np.arange(0, c.head_dim, 2).astype(np.float32)
+    rinv = np.float32(1.0) / np.float32(c.rotary_dim)
+    f = np.power(np.float32(c.rope_theta), -(j * rinv).astype(np.float32)).astype(np.float32)
     f[j >= c.rotary_dim] = 0.0
     return f.astype(np.float32)
 
