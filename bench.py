@@ -404,6 +404,31 @@ def tp_bytes_per_token(cfg, size):
     return cfg.n_layers * per_layer + cfg.dim * wb + cfg.dim * 4 + cfg.vocab_size // size * cfg.dim * wb
 
 
+def graph_kernels(dec):
+    """Kernel launches per greedy token (the captured graph's kernel nodes); None when the
+    decoder launches eagerly (YALM_EAGER=1 under the profiler)."""
+    try:
+        return dec.graph_kernels(2)
+    except Exception:
+        return None
+
+
+def tp_info(mode, exch_us, kernels, cfg, agree):
+    """The line's `tp` object. RCCL: 2 all-reduces per layer + the argmax gather, each
+    its own collective launch (exchange_us = one all-reduce of x). IPC (tp_exchange.h): no
+    exchange launches -- each exchange is pushed by its producer (Wo / W2 / argmax) and
+    summed inside its consumer's x staging (exchange_us = the consumer side alone, timed as
+    a launch of its own: an upper bound of what the folded form adds)."""
+    n_ex = 2 * cfg.n_layers + 1
+    out = {"exchange_us": round(exch_us, 3), "exchanges_per_token": n_ex, "kernels_per_token": kernels,
+           "ranks_agree": agree}
+    if mode == "tp-ipc":
+        out["exchange_form"] = "folded into the producer and consumer kernels (no exchange launches)"
+    else:
+        out["exchange_ms_per_token"] = round(exch_us * n_ex / 1e3, 4)
+    return out
+
+
 def make_decoder(runtime, M, cfg, rank, world, mode, dist):
     """(DeviceModel, Decoder) for mode "single" | "replica" | "tp-rccl" | "tp-ipc"."""
     if mode in ("single", "replica"):
@@ -566,6 +591,7 @@ def main():
     kname = dec.kernel_name(KID)
     traffic, traffic_src = pmc_traffic((f"gemv_rb_kernel<{wt}", "PGlu"))
     exch_us = None
+    kernels_per_token = graph_kernels(dec)
     if tp and tp_size > 1:
         exch_us = dec.time_kernel(6, args.kernel_iters) * 1e3
     env_ms = None
@@ -635,13 +661,9 @@ def main():
         "gpu_state": state,
         "cpu_baseline": None,
     }
+    out["kernels_per_token"] = kernels_per_token
     if tp and tp_size > 1:
-        out["tp"] = {
-            "exchange_us": round(exch_us, 3),
-            "exchanges_per_token": 2 * cfg.n_layers + 1,
-            "exchange_ms_per_token": round(exch_us * (2 * cfg.n_layers + 1) / 1e3, 4),
-            "ranks_agree": agree,
-        }
+        out["tp"] = tp_info(mode, exch_us, kernels_per_token, cfg, agree)
     if fallback:
         out["fallback"] = fallback
     dec.close()
@@ -658,16 +680,18 @@ def main():
         try:
             dm, dec = make_decoder(runtime, M, cfg, rank, world, "tp-ipc", dist)
             e2, _, _, agree2 = timed_decode(dec, True)
+            k2 = graph_kernels(dec)
             ex2 = dec.time_kernel(6, args.kernel_iters) * 1e3
             out["tp_ipc"] = {"value": round(args.steps / e2, 3), "ms_per_step": round(e2 / args.steps * 1e3, 4),
-                             "exchange_us": round(ex2, 3), "ranks_agree": agree2}
+                             "exchange_us": round(ex2, 3), "kernels_per_token": k2, "ranks_agree": agree2}
             dec.close()
             dm.close()
             if agree2 and e2 < elapsed:
                 # the line's value is the faster measured transport (both measured in this run,
                 # same workload, same barriers and max-over-ranks clock); the other stays beside it
                 out["tp_rccl"] = {"value": out["value"], "ms_per_step": out["ms_per_step"],
-                                  "exchange_us": out["tp"]["exchange_us"], "ranks_agree": out["tp"]["ranks_agree"]}
+                                  "exchange_us": out["tp"]["exchange_us"],
+                                  "kernels_per_token": out["kernels_per_token"], "ranks_agree": out["tp"]["ranks_agree"]}
                 del out["tp_ipc"]
                 out["value"] = round(args.steps / e2, 3)
                 out["ms_per_step"] = round(e2 / args.steps * 1e3, 4)
@@ -675,9 +699,9 @@ def main():
                 out["step_roofline"]["achieved_per_gpu"] = round(gbs, 1)
                 out["step_roofline"]["frac"] = round(gbs / HBM_PEAK_GBS, 4)
                 out["config"]["parallelism"] = f"tp{tp_size}-ipc"
-                out["tp"] = {"exchange_us": round(ex2, 3), "exchanges_per_token": 2 * cfg.n_layers + 1,
-                             "exchange_ms_per_token": round(ex2 * (2 * cfg.n_layers + 1) / 1e3, 4),
-                             "ranks_agree": agree2, "transport": "ipc (faster of the two measured)"}
+                out["kernels_per_token"] = k2
+                out["tp"] = tp_info("tp-ipc", ex2, k2, cfg, agree2)
+                out["tp"]["transport"] = "ipc (faster of the two measured)"
         except Exception as e:  # report, never hide
             out["tp_ipc"] = {"error": str(e)[:200]}
     if fp8_leg_out is not None:

@@ -160,6 +160,11 @@ int yalm_stream_envelope(size_t bytes, int iters, float *avg_ms);
  * workgroups per CU of the row-block kernel; 0 = automatic.
  * Drops captured graphs (re-captured on next use). Tuning/ablation hook. */
 int yalm_set_gemv_config(yalm_decoder d, int kind, int threads, int unroll, int gpw);
+/* Kernel launches per forward of graph `mode` (0 = HYDRATE, 1 = OUTPUT_LOGITS, 2 = the
+ * device greedy step): *kernels = kernel nodes of the captured per-token hipGraph (RCCL
+ * collectives count as the kernels they capture), *nodes (may be NULL) = all nodes. Test
+ * and measurement hook (tensor parallelism adds no exchange launches over IPC). */
+int yalm_graph_kernels(yalm_decoder d, int mode, int *kernels, int *nodes);
 /* Name of kernel_id's device function (to match rocprofv3 summaries). */
 const char *yalm_kernel_name(yalm_decoder d, int kernel_id);
 /* 1 if this decoder's launch path runs attention and the Wo projection (+ the

@@ -69,7 +69,8 @@ def test_attn_wo_plan_host_arithmetic():
     slots (2 per CU x 256) fuses with the key splits that fit beside the mergers and the
     Wo workgroups; a dim-8192 model (512 Wo workgroups) leaves fewer than 2
     splits, so it keeps the separate launches instead of running every context in head
-    mode; shapes outside the fused contract (head_dim 64, Wo rows of 2 KB) never fuse."""
+    mode; the per-rank configs of Mistral TP2/4/8 (Wo rows of 4, 2, 1 KiB) fuse; shapes
+    outside the fused contract (head_dim 64, Wo rows of 512 B) never fuse."""
     from yalm_amd import models as M
     from yalm_amd import runtime
 
@@ -81,7 +82,13 @@ def test_attn_wo_plan_host_arithmetic():
     ok, S, _ = runtime.attn_wo_plan(big.with_(max_seq_len=256), 512)
     assert ok and S == 1
     assert runtime.attn_wo_plan(M.MISTRAL_7B.with_(head_dim=64, n_heads=64, n_kv_heads=16), 512)[0] is False
-    assert runtime.attn_wo_plan(M.MISTRAL_7B.with_(n_heads=8, n_kv_heads=2), 512)[0] is False
+    for tp in (2, 4, 8):
+        local = M.MISTRAL_7B.with_(n_heads=32 // tp, n_kv_heads=8 // tp, hidden_dim=14336 // tp,
+                                   vocab_size=32000 // tp)
+        ok, S, grid = runtime.attn_wo_plan(local, 512)
+        assert ok and 2 <= S <= 32 and grid <= 512, (tp, S, grid)
+    assert runtime.attn_wo_plan(M.MISTRAL_7B.with_(n_heads=2, n_kv_heads=2), 512)[0] is False
+    assert runtime.attn_wo_plan(M.MISTRAL_7B.with_(n_heads=4, n_kv_heads=1, weight_dtype=M.F8E5M2), 512)[0] is False
 
 
 def test_prefill_forms_spec_validation():

@@ -161,3 +161,25 @@ def test_cli_completion_prefill_same_tokens(host_built, tmp_path):
         return line
 
     assert toks({}) == toks({"YALM_NO_PREFILL": "1"})
+
+
+@pytest.mark.gpu
+def test_cli_passkey_prefill_matches_sequential(host_built, tmp_path):
+    """-m passkey (main.cpp:202-288): the in-window prompt positions hydrated by one batched
+    prefill, the rest (a -T 128 window: past max_seq_len, sliding window + sinks) and the
+    answer one forward each -- the same 16 answer tokens as the all-forward run
+    (YALM_NO_PREFILL=1); the passkey value is fixed by YALM_SEED."""
+    path = _prefill_yalm(tmp_path)
+    exe = os.path.join(host_built, "yalm")
+
+    def run(extra_env):
+        r = subprocess.run([exe, path, "-d", "hip", "-m", "passkey", "-n", "6", "-l", "2", "-T", "128"],
+                           capture_output=True, env=dict(os.environ, YALM_PRINT_TOKENS="1", YALM_SEED="7", **extra_env),
+                           timeout=120)
+        assert r.returncode == 0, r.stderr.decode()
+        out = r.stdout.decode()
+        m = re.search(r"prompt: (\d+) tokens", out)
+        assert m and int(m.group(1)) > 128, out  # the prompt runs past the window
+        return [l for l in r.stderr.decode().split("\n") if l.startswith("TOKENS:")][0]
+
+    assert run({}) == run({"YALM_NO_PREFILL": "1"})

@@ -32,13 +32,24 @@
 // forward stopped part-way) stays correct. Every spin is bounded and reports in
 // *err.
 //
-// Geometry: Wo rows are q_dim * BYTES = XS * 4 KB (XS in {1, 2}); Wo workgroup
-// j owns rows [j * AWO_RPW, j * AWO_RPW + AWO_RPW) and thread t loads 16-byte
-// pieces i * 256 + t of that contiguous slice (LPT = AWO_RPW * XS loads).
+// Geometry: Wo rows are q_dim * BYTES = KB KiB (KB in {1, 2, 4, 8}: 4 and 8 on one GPU
+// at Mistral / Llama shapes, 2 and 1 for the per-rank Wo of tensor parallelism); Wo
+// workgroup j owns rows [j * AWO_RPW, j * AWO_RPW + AWO_RPW) and thread t loads 16-byte
+// pieces i * 256 + t of that contiguous slice (LPT = AWO_RPW * KB / 4 loads). KB >= 4: a
+// thread's pieces cover every row of the slice, KB / 4 column pieces each; KB < 4: a
+// 4-KiB load instruction covers RPL = 4 / KB rows, so a thread covers every RPL-th row
+// at ONE column piece (256 / RPL threads per row).
+//
+// Outputs (round 5): x[row] = x + Wo v on one GPU; under tensor parallelism over RCCL
+// the partial (+ x on rank 0) goes to out = xs for the all-reduce; over IPC it is pushed
+// to every rank's exchange slot (tp_exchange.h) and the launch's last Wo workgroup bumps
+// the exchange count -- the attention + Wo launch IS the exchange's producer, and the
+// GLU GEMV after it the consumer.
 #pragma once
 
 #include "attention.h"
 #include "device_common.h"
+#include "tp_exchange.h"
 
 #define AWO_RPW 16                   // Wo rows per Wo workgroup (256 of them for Mistral-7B)
 #define AWO_TIMEOUT 200000000ull     // 2 s of s_memrealtime (100 MHz)
@@ -53,7 +64,10 @@ struct AttnWoArgs {
 	int layer, n_layers;      // partial tag = epoch * n_layers + layer (attention.h)
 	const unsigned long long *gran; // this layer's attention output (q_dim) as {value, epoch} granules
 	const char *wo;     // Wo (dim, q_dim)
-	float *x;           // residual stream (dim)
+	float *x;           // residual stream (dim): read for the residual when add_base
+	float *out;         // x (one GPU), xs (RCCL partial) -- unused when push.n > 0
+	int add_base;       // out = x + Wo v (one GPU, TP rank 0) or Wo v (other TP ranks)
+	TpX push;           // IPC tensor parallelism: push.n > 0 pushes the rows (tp_exchange.h)
 	unsigned *err;      // error bits (bounded spin gave up)
 	unsigned long long *trace; // [grid][AWO_TRACE_N] s_memrealtime stamps (YALM_ATTN_WO_TRACE=1) or null
 	int delay;          // s_memrealtime ticks (10 ns) the Wo workgroups wait before their slice loads
@@ -101,21 +115,23 @@ __device__ __forceinline__ void awo_ld8_sc1(u32x4_t (&v)[8], const void *const (
 // stale tag) slower again: fp8 kv 17 7.40 -> 8.49 us, kv 100 8.86 -> 11.68
 // (profiles/r4k_decode_ab.txt). False if the bounded spin gave up (deadline,
 // s_memrealtime).
+// XS pieces of EPL columns each: piece k of this thread starts at column
+// (piece0 + 256 k) * EPL; wpiece0 = piece0 of the wave's lane 0 (the sentinel heads).
 template <int EPL, int XS>
-__device__ __forceinline__ bool awo_gather_gran(float (&xs)[XS][EPL], const unsigned long long *gran, int tid,
-                                                unsigned tag, unsigned long long deadline) {
+__device__ __forceinline__ bool awo_gather_gran(float (&xs)[XS][EPL], const unsigned long long *gran, int piece0,
+                                                int wpiece0, unsigned tag, unsigned long long deadline) {
 	constexpr int LPP = EPL / 2;   // 16-byte loads per piece
 	constexpr int NL = XS * LPP;   // 4, 8 or 16
 	constexpr int NB = (NL + 7) / 8;
 	constexpr int D = 128;
 	constexpr int HPP = 64 * EPL / D; // heads per piece (4 or 8)
 	bool alive = true;
-	const int lane = tid & 63, wave = tid >> 6;
+	const int lane = threadIdx.x & 63;
 	const unsigned long long *sent;
 	{
 		const int l = lane < XS * HPP ? lane : 0;
 		const int k = l / HPP;
-		const int h = (k * ATTN_THREADS + 64 * wave) * EPL / D + l % HPP;
+		const int h = (k * ATTN_THREADS + wpiece0) * EPL / D + l % HPP;
 		sent = gran + (size_t)h * D + (D - 1);
 	}
 	asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the slice has landed
@@ -136,7 +152,7 @@ __device__ __forceinline__ bool awo_gather_gran(float (&xs)[XS][EPL], const unsi
 		for (int i = 0; i < 8; ++i) {
 			const int l = bt * 8 + (i < NL - bt * 8 ? i : 0); // pad a short batch with a repeat
 			const int k = l / LPP, e = (l % LPP) * 2;
-			a[i] = gran + (size_t)(k * ATTN_THREADS + tid) * EPL + e;
+			a[i] = gran + (size_t)(k * ATTN_THREADS + piece0) * EPL + e;
 		}
 		u32x4_t v[8];
 		for (;;) {
@@ -165,15 +181,19 @@ __device__ __forceinline__ bool awo_gather_gran(float (&xs)[XS][EPL], const unsi
 	return alive;
 }
 
-template <class WT, int GT, int XS>
+template <class WT, int GT, int KB>
 __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__restrict__ q,
                                                                const uint16_t *__restrict__ kc,
                                                                const uint16_t *__restrict__ vc,
                                                                const StepState *__restrict__ step, AttnWoArgs p) {
 	constexpr int D = 128;
 	constexpr int EPL = WT::EPL;
-	constexpr int LPT = AWO_RPW * XS;
+	constexpr int XS = KB >= 4 ? KB / 4 : 1;   // column pieces per thread
+	constexpr int RPL = KB >= 4 ? 1 : 4 / KB;  // rows per 4-KiB load instruction
+	constexpr int TPR = ATTN_THREADS / RPL;    // threads per row (KB < 4)
+	constexpr int LPT = AWO_RPW * KB / 4;      // 16-byte loads per thread
 	static_assert(ATTN_THREADS == 256 && ATTN_WAVES == 4, "4-wave workgroups: one 4-row reduction per wave");
+	static_assert(KB == 1 || KB == 2 || KB == 4 || KB == 8, "Wo rows of 1, 2, 4 or 8 KiB");
 	const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 	const int G = p.n_heads / p.n_kv;
 	const int units = p.n_kv * (p.S + G - 1); // attention workgroups (head units + split units)
@@ -214,7 +234,9 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 	const char *wbase = p.wo + (size_t)lrow0 * p.q_dim * WT::BYTES;
 	// the residual rows this workgroup adds to, loaded first (nothing else in the launch
 	// writes x): the read-modify-write at the end costs no load round trip
-	const float xres = p.x[lrow0 + (tid & (AWO_RPW - 1))];
+	const float xres = p.add_base ? p.x[lrow0 + (tid & (AWO_RPW - 1))] : 0.0f;
+	const bool push = p.push.n > 0;
+	const unsigned par = push ? tpx_seq(p.push) & 1u : 0u; // exchange parity, read ahead of the stream
 	if (p.delay > 0) {
 		const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 		while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)p.delay)
@@ -235,35 +257,62 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 	// only for the heads its columns cover), then dot them into every resident row.
 	const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 	float xs[XS][EPL];
-	if (!awo_gather_gran<EPL, XS>(xs, p.gran, tid, epoch, t0 + AWO_TIMEOUT) && lane == 0)
+	const int piece0 = KB >= 4 ? tid : tid % TPR, wpiece0 = KB >= 4 ? 64 * wave : (64 * wave) % TPR;
+	if (!awo_gather_gran<EPL, XS>(xs, p.gran, piece0, wpiece0, epoch, t0 + AWO_TIMEOUT) && lane == 0)
 		__hip_atomic_fetch_or(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 	if (tr)
 		t_poll = __builtin_amdgcn_s_memrealtime(), c_poll = __builtin_amdgcn_s_memtime();
-	float a0[AWO_RPW], a1[AWO_RPW];
+	if constexpr (KB >= 4) {
+		float a0[AWO_RPW], a1[AWO_RPW];
 #pragma unroll
-	for (int r = 0; r < AWO_RPW; ++r) {
-		a0[r] = a1[r] = 0.0f;
+		for (int r = 0; r < AWO_RPW; ++r) {
+			a0[r] = a1[r] = 0.0f;
 #pragma unroll
-		for (int k = 0; k < XS; ++k)
-			dot16_mix<WT>(a0[r], a1[r], wr[r * XS + k], xs[k]);
-	}
-	// ---- resident rows . slice; 4-row transposed wave reductions; fixed-order workgroup sum
+			for (int k = 0; k < XS; ++k)
+				dot16_mix<WT>(a0[r], a1[r], wr[r * XS + k], xs[k]);
+		}
+		// ---- resident rows . slice; 4-row transposed wave reductions; fixed-order workgroup sum
 #pragma unroll
-	for (int r0 = 0; r0 < AWO_RPW; r0 += 4) {
-		float acc[4];
+		for (int r0 = 0; r0 < AWO_RPW; r0 += 4) {
+			float acc[4];
 #pragma unroll
-		for (int t = 0; t < 4; ++t)
-			acc[t] = a0[r0 + t] + a1[r0 + t];
-		const float tot = sum4_t(acc); // lanes 16 g .. 16 g + 15: row r0 + g
-		if ((lane & 15) == 0)
-			rowpart[r0 + (lane >> 4)][wave] = tot;
+			for (int t = 0; t < 4; ++t)
+				acc[t] = a0[r0 + t] + a1[r0 + t];
+			const float tot = sum4_t(acc); // lanes 16 g .. 16 g + 15: row r0 + g
+			if ((lane & 15) == 0)
+				rowpart[r0 + (lane >> 4)][wave] = tot;
+		}
+	} else {
+		// load i holds row i * RPL + tid / TPR at column piece tid % TPR: per-wave totals of 4
+		// loads at a time (sum4_t), then (RPL 2: two waves per row) the waves of a row in LDS
+#pragma unroll
+		for (int i0 = 0; i0 < LPT; i0 += 4) {
+			float acc[4];
+#pragma unroll
+			for (int t = 0; t < 4; ++t) {
+				float a0 = 0.0f, a1 = 0.0f;
+				dot16_mix<WT>(a0, a1, wr[i0 + t], xs[0]);
+				acc[t] = a0 + a1;
+			}
+			const float tot = sum4_t(acc); // lanes 16 g .. 16 g + 15: load i0 + g
+			if ((lane & 15) == 0) {
+				const int i = i0 + (lane >> 4);
+				rowpart[i * RPL + tid / TPR][RPL == 4 ? 0 : (wave & 1)] = tot;
+			}
+		}
 	}
 	__syncthreads();
 	const int row = lrow0 + tid;
 	if (tid < AWO_RPW && row >= row0) {
-		const float s = (rowpart[tid][0] + rowpart[tid][1]) + (rowpart[tid][2] + rowpart[tid][3]);
-		p.x[row] = xres + s;
+		const float s = KB >= 4 ? (rowpart[tid][0] + rowpart[tid][1]) + (rowpart[tid][2] + rowpart[tid][3])
+		                        : (RPL == 4 ? rowpart[tid][0] : rowpart[tid][0] + rowpart[tid][1]);
+		if (push)
+			tpx_put(p.push, par, row, xres + s);
+		else
+			p.out[row] = xres + s;
 	}
+	if (push) // this launch's Wo workgroups produce the exchange: the last one bumps the counts
+		tpx_arrive(p.push, (p.dim + AWO_RPW - 1) / AWO_RPW);
 	if (tr) {
 		tr[3] = __builtin_amdgcn_s_memrealtime(), tr[11] = __builtin_amdgcn_s_memtime();
 		tr[0] = t_start, tr[8] = c_start, tr[1] = t_slice, tr[9] = c_slice, tr[2] = t_poll, tr[10] = c_poll;
@@ -271,4 +320,3 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 			tr[k] = tr[8 + k] = 0;
 	}
 }
-

@@ -10,6 +10,7 @@
 
 #include "../../include/yalm_hip.h"
 #include "device_common.h"
+#include "tp_exchange.h"
 
 // ------------------------------------------------------------------ errors
 void set_err(const std::string &s); // yalm_hip.hip (thread-local last error)
@@ -128,18 +129,22 @@ struct yalm_decoder_s {
 	float *logits_local = nullptr;   // [vocab / tp] this rank's logits rows (== logits without TP)
 	float *amax = nullptr;           // [2] local argmax (value, global index as float bits)
 	float *amax_all = nullptr;       // [2 * tp_size]
-	// IPC one-shot exchange transport (yalm_decoder_create_tp_ipc): every rank's
-	// buffer [2 slots x ipc_S floats][flags: 64 u32][seq u32] mapped on all ranks
+	// IPC transport (yalm_decoder_create_tp_ipc, tp_exchange.h): every rank's uncached
+	// buffer [2 parities][tp_size][ipc_S floats][control words] mapped on all ranks; the
+	// exchanges are folded into their producer and consumer kernels (no exchange launch)
 	bool ipc = false;
-	int ipc_S = 0;                   // floats per slot
+	int ipc_S = 0;                   // floats per (parity, source) slot
 	float *ipc_own = nullptr;        // this rank's buffer
 	float **ipc_bufs = nullptr;      // device array [tp_size] of buffer bases (peers opened via IPC)
 	std::vector<void *> ipc_opened;  // hipIpcOpenMemHandle mappings to close
+	TpX tpx{};                       // the exchange descriptor passed to producers / consumers
+	bool tpx_gate = false;           // ranks share this GPU: a 1-wave wait launch before each consumer
 	// launch path: attention + Wo as one launch (attn_wo.h) when supported;
 	// YALM_ATTN_WO=0 selects the two separate kernels
 	bool attn_wo = false;
 	int awo_nb = 0;                  // grid: n_kv * (awo_S + G - 1) attention + n_heads mergers + ceil(dim / AWO_RPW) Wo
 	int awo_S = 0;                   // key-chunk splits per kv head
+	int awo_slots = 0;               // co-resident workgroup slots of the fused launch (occupancy x CUs)
 	unsigned long long *awo_trace = nullptr; // A/B build, YALM_ATTN_WO_TRACE=1: [grid][16] stamps of the last launch
 	int awo_delay = 0;               // ticks the Wo workgroups wait before their slice loads
 	unsigned long long *awo_gran = nullptr; // [n_layers][q_dim] attention outputs as {value, epoch} granules

@@ -49,6 +49,18 @@ __device__ __forceinline__ float xor32(float v) {
 	auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
 	return __builtin_bit_cast(float, (threadIdx.x & 32) ? r[0] : r[1]);
 }
+// ss + v0^2 + v1^2 + v2^2 + v3^2 as an explicit fma chain: the x staging of the GEMV
+// (gemv.h) and of the tensor-parallel exchange consumer (tp_exchange.h) must round
+// identically (TP1 is bit-exact vs one GPU), and hipcc contracts a written-out sum of
+// products differently depending on the surrounding code.
+__device__ __forceinline__ float sumsq4(float ss, const float4_t &v) {
+	float t = v[0] * v[0];
+	t = __builtin_fmaf(v[1], v[1], t);
+	t = __builtin_fmaf(v[2], v[2], t);
+	t = __builtin_fmaf(v[3], v[3], t);
+	return ss + t;
+}
+
 // Sum / max over each aligned row of 16 lanes (result in every lane of the row):
 // quad_perm [1,0,3,2] (xor 1), [2,3,0,1] (xor 2), row_half_mirror, row_mirror.
 __device__ __forceinline__ float row16_sum(float v) {

@@ -18,6 +18,7 @@
 #include <type_traits>
 
 #include "device_common.h"
+#include "tp_exchange.h"
 
 #define GEMV_THREADS 256
 
@@ -109,38 +110,48 @@ struct PAddTo {
 	}
 };
 
-// IPC tensor-parallel partial: out = slot buffer chosen at run time by the
-// exchange sequence number (slot (seq + 1) & 1 of this rank's IPC buffer, so
-// consecutive exchanges alternate slots whatever graph runs), rank 0 adding
-// the residual base (x) as PAddTo does.
+// IPC tensor-parallel producer (tp_exchange.h): row value (+ the residual base on rank 0)
+// pushed into this rank's slot of every rank's exchange buffer, at element offset + row;
+// the launch's last workgroup then bumps this rank's exchange count everywhere (tail).
 template <class WT, int R_>
-struct PSlot {
+struct PPush {
 	static constexpr int R = R_;
 	const char *W;
 	int n;
-	float *slots;        // this rank's IPC buffer
-	int S, offset;       // floats per slot, offset inside the slot
-	const unsigned *seq; // exchange sequence counter (in the IPC buffer)
-	const float *base;   // residual (rank 0) or null
+	const float *base; // residual (rank 0's x) or null
+	TpX t;
+	int offset;
 	int n_groups;
-	__device__ __forceinline__ void prologue() const {}
+	mutable unsigned par = 0; // parity of this exchange (read in prologue, ahead of the stream's end)
+	__device__ __forceinline__ void prologue() const { par = tpx_seq(t) & 1u; }
 	__device__ __forceinline__ const char *row(int g, int r) const {
 		return W + (size_t)(g * R + r) * n * WT::BYTES;
 	}
-	__device__ __forceinline__ float *out() const {
-		return slots + (size_t)((*seq + 1u) & 1u) * S + offset;
-	}
-	__device__ __forceinline__ void finish(int g, const float *acc, int lane) const {
-		if (lane < R)
-			out()[g * R + lane] = (base ? base[g * R + lane] : 0.0f) + acc[lane];
-	}
-	__device__ __forceinline__ void finish_all(int g, const float *acc) const {
-		float *o = out();
+	static constexpr bool PRE = true;
+	__device__ __forceinline__ float pre(int g, int r) const { return base ? base[g * R + r] : 0.0f; }
+	__device__ __forceinline__ void finish_pre(int g, const float *acc, const float *xr) const {
 #pragma unroll
 		for (int r = 0; r < R; ++r)
-			o[g * R + r] = (base ? base[g * R + r] : 0.0f) + acc[r];
+			tpx_put(t, par, offset + g * R + r, xr[r] + acc[r]);
 	}
+	__device__ __forceinline__ void finish_all(int g, const float *acc) const {
+#pragma unroll
+		for (int r = 0; r < R; ++r)
+			tpx_put(t, par, offset + g * R + r, (base ? base[g * R + r] : 0.0f) + acc[r]);
+	}
+	__device__ __forceinline__ void finish(int g, const float *acc, int lane) const { // gemv_kernel
+		if (lane < R)
+			tpx_put(t, par, offset + g * R + lane, (base ? base[g * R + lane] : 0.0f) + acc[lane]);
+	}
+	static constexpr bool TAIL = true;
+	__device__ __forceinline__ void tail() const { tpx_arrive(t, gridDim.x); }
 };
+
+// policies with a tail() every thread runs after the epilogues (TAIL = true)
+template <class P, class = void>
+struct gemv_tail : std::false_type {};
+template <class P>
+struct gemv_tail<P, std::void_t<decltype(P::TAIL)>> : std::bool_constant<P::TAIL> {};
 
 // Virtual row space [wq | wk | wv]; a wave owns the RoPE pair (2g, 2g+1).
 template <class WT>
@@ -255,7 +266,7 @@ __device__ __forceinline__ void stage_x(float *xs, const float *__restrict__ x, 
 		float ss = 0.0f;
 		for (int i = tid * 4; i < n; i += nthreads * 4) {
 			float4_t v = *(const float4_t *)(x + i);
-			ss += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+			ss = sumsq4(ss, v);
 		}
 		ss = wave_sum(ss);
 		if ((tid & 63) == 0)
@@ -322,7 +333,7 @@ __device__ __forceinline__ void stage_x_regs(float *xs, const XPre<NORM, THREADS
 		for (int k = 0; k < xpre_n<NORM, THREADS>(); ++k) {
 			if ((tid + k * nthreads) * 4 < n) {
 				const float4_t v = r.x[k];
-				ss += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+				ss = sumsq4(ss, v);
 			}
 		}
 		ss = wave_sum(ss);
@@ -439,6 +450,8 @@ __global__ __launch_bounds__(GEMV_THREADS) void gemv_kernel(P p, const float *__
 			acc[r] = wave_sum(acc[r]);
 		p.finish(g, acc, lane);
 	}
+	if constexpr (gemv_tail<P>::value)
+		p.tail();
 }
 
 // Row-block GEMV — the production path (n % (64 * EPL) == 0).
@@ -463,9 +476,14 @@ __global__ __launch_bounds__(GEMV_THREADS) void gemv_kernel(P p, const float *__
 // chunks of its rows, so the wave reduction runs once per row instead of once per 1-KB
 // chunk (W1|W3 at n 4096: 8 reductions per row -> 1; tools/pattern_bench.hip: the chunk
 // order with its per-chunk work ran 10-25% below the streaming envelope, whole rows at it).
+//
+// TIN (tensor parallelism over IPC, tp_exchange.h): tin.n > 0 makes this launch the
+// consumer of an exchange -- x is the rank-order sum of every rank's pushed partial,
+// waited for and summed AFTER the first weight loads are issued, so the exchange latency
+// runs under the weight stream's start instead of in a launch of its own.
 template <class WT, class P, int U, bool NORM, int THREADS, bool ROWS = false>
 __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__restrict__ x,
-                                                          const float *__restrict__ normw, float eps) {
+                                                          const float *__restrict__ normw, float eps, TpX tin) {
 	extern __shared__ __attribute__((aligned(16))) float xs[];
 	constexpr int R = P::R;
 	constexpr int EPL = WT::EPL;
@@ -511,7 +529,8 @@ __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__re
 
 	int ivr = ROWS ? wave : wave / nch, ic = ROWS ? 0 : wave - (wave / nch) * nch; // issue cursor
 	const int vr0 = ivr, c0 = ic;
-	const bool xregs = n <= 4 * xpre_n<NORM, THREADS>() * THREADS; // x (+ norm weights) fit the registers
+	const bool tpx = tin.n > 0;                                      // x from an exchange (uniform)
+	const bool xregs = !tpx && n <= 4 * xpre_n<NORM, THREADS>() * THREADS; // x (+ norm weights) fit the registers
 	XPre<NORM, THREADS> xp;
 	if (xregs)
 		prefetch_x<NORM, THREADS>(xp, x, normw, n); // ahead of the weight stream in vmcnt order
@@ -531,7 +550,9 @@ __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__re
 	p.prologue();
 	for (int i = threadIdx.x; i < ngl * R * W; i += THREADS)
 		part[i] = 0.0f;
-	if (xregs)
+	if (tpx)
+		tpx_stage_x<NORM>(xs, tin, tpx_wait(tin), normw, n, eps);
+	else if (xregs)
 		stage_x_regs<NORM, THREADS>(xs, xp, n, eps);
 	else
 		stage_x<NORM>(xs, x, normw, n, eps);
@@ -583,6 +604,8 @@ __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__re
 			p.finish_all(b + gl * NB, a);
 		}
 	}
+	if constexpr (gemv_tail<P>::value)
+		p.tail();
 #ifdef YALM_WG_TRACE // tools/wg_timeline.hip: per-workgroup start/end (s_memrealtime, 100 MHz)
 	if (threadIdx.x == 0) {
 		yalm_wg_trace[2 * b] = t_start;

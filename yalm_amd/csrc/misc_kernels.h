@@ -5,6 +5,7 @@
 #include <float.h>
 
 #include "device_common.h"
+#include "tp_exchange.h"
 
 // Host-provided (token, pos) -> device StepState. Launched eagerly ahead of a
 // graph replay; kernel arguments are captured at launch, so no host buffer race.
@@ -56,16 +57,8 @@ __global__ __launch_bounds__(256) void step_begin_kernel(StepState *st, const vo
 
 // Greedy sampling on the device (sampler.cpp:27-38: strict '>' scan, so the
 // FIRST maximum wins). Feeds the result back as the next step's token.
-__global__ __launch_bounds__(1024) void argmax_kernel(const float *__restrict__ logits, int n, StepState *st,
-                                                      int *__restrict__ tokens_out, int cap,
-                                                      float *__restrict__ pair_out = nullptr, int index_offset = 0,
-                                                      const unsigned *__restrict__ slot_seq = nullptr,
-                                                      int slot_floats = 0) {
-	if (slot_seq) { // IPC transport: logits and the pair live in slot (seq + 1) & 1
-		const size_t so = (size_t)((*slot_seq + 1u) & 1u) * slot_floats;
-		logits += so;
-		pair_out += so;
-	}
+// First max of logits[0, n) over one workgroup of 1024 threads: (value, index) in thread 0.
+__device__ __forceinline__ void argmax_block(const float *__restrict__ logits, int n, float &best_out, int &idx_out) {
 	__shared__ float sv[16];
 	__shared__ int si[16];
 	float best = -FLT_MAX;
@@ -128,17 +121,94 @@ __global__ __launch_bounds__(1024) void argmax_kernel(const float *__restrict__ 
 		}
 		if (idx == 0x7fffffff)
 			idx = 0; // all -FLT_MAX / NaN: the reference returns 0
-		if (pair_out) { // tensor-parallel shard: publish (value, global index) for argmax_pick_kernel
+		best_out = b;
+		idx_out = idx;
+	}
+}
+
+// the device greedy loop's bookkeeping: token `idx` is the next step's input
+__device__ __forceinline__ void argmax_commit(StepState *st, int idx, int *__restrict__ tokens_out, int cap) {
+	const int k = st->n_gen;
+	if (tokens_out && k < cap)
+		tokens_out[k] = idx;
+	st->n_gen = k + 1;
+	st->token = idx;
+	st->pos = st->pos + 1;
+}
+
+__global__ __launch_bounds__(1024) void argmax_kernel(const float *__restrict__ logits, int n, StepState *st,
+                                                      int *__restrict__ tokens_out, int cap,
+                                                      float *__restrict__ pair_out = nullptr, int index_offset = 0) {
+	float b = 0.0f;
+	int idx = 0;
+	argmax_block(logits, n, b, idx);
+	if (threadIdx.x == 0) {
+		if (pair_out) { // tensor-parallel shard (RCCL): publish (value, global index) for argmax_pick_kernel
 			pair_out[0] = b;
 			pair_out[1] = __int_as_float(idx + index_offset);
 			return;
 		}
-		const int k = st->n_gen;
-		if (tokens_out && k < cap)
-			tokens_out[k] = idx;
-		st->n_gen = k + 1;
-		st->token = idx;
-		st->pos = st->pos + 1;
+		argmax_commit(st, idx, tokens_out, cap);
+	}
+}
+
+// Tensor parallelism over IPC (tp_exchange.h): this rank's first max over its vocabulary
+// slice [rank * n, (rank + 1) * n) is pushed as a (value, global index) pair to every rank,
+// then the kernel waits for every rank's pair and picks the global first max in rank order
+// (ranks own ascending slices: ties resolve to the lowest index, sampler.cpp:27-38) --
+// the exchange and the pick inside the argmax launch, identical on every rank.
+__global__ __launch_bounds__(1024) void argmax_tp_kernel(const float *__restrict__ logits, int n, StepState *st,
+                                                         int *__restrict__ tokens_out, int cap, TpX t) {
+	float b = 0.0f;
+	int idx = 0;
+	argmax_block(logits, n, b, idx);
+	if (threadIdx.x == 0) {
+		const unsigned par = tpx_seq(t) & 1u;
+		tpx_put(t, par, 0, b);
+		tpx_put(t, par, 1, __int_as_float(idx + t.rank * n));
+	}
+	tpx_arrive(t, 1);
+	if (threadIdx.x < 64) {
+		const unsigned par = tpx_wait(t);
+		if (threadIdx.x == 0) {
+			float bb = 0.0f;
+			int bi = 0;
+			for (int p = 0; p < t.n; ++p) {
+				const float *pr = t.slot(t.rank, par, p);
+				const float v = tpx_ldf(pr);
+				const int j = __float_as_int(tpx_ldf(pr + 1));
+				if (p == 0 || v > bb || (v == bb && j < bi)) {
+					bb = v;
+					bi = j;
+				}
+			}
+			argmax_commit(st, bi, tokens_out, cap);
+		}
+	}
+}
+
+// Tensor parallelism over IPC, ranks sharing one GPU: wait for the exchange in one wave
+// before the consumer launch (yalm_hip.hip tpx_consume).
+__global__ __launch_bounds__(64) void tpx_gate_kernel(TpX t) {
+	(void)tpx_wait(t);
+}
+
+// Tensor parallelism over IPC: the consumer side of one exchange as a launch of its own --
+// the summed x into `out` (yalm_block's result; the timing hook of the exchange), or, with
+// gather, the n floats of every rank's slot side by side (the sharded logits).
+__global__ __launch_bounds__(1024) void tpx_collect_kernel(TpX t, int n, int gather, float *__restrict__ out) {
+	const unsigned par = tpx_wait(t);
+	if (gather) {
+		for (int p = 0; p < t.n; ++p)
+			for (int i = threadIdx.x; i < n; i += blockDim.x)
+				out[(size_t)p * n + i] = tpx_ldf(t.slot(t.rank, par, p) + i);
+		return;
+	}
+	for (int i = threadIdx.x; i < n; i += blockDim.x) {
+		float s = tpx_ldf(t.slot(t.rank, par, 0) + i);
+		for (int p = 1; p < t.n; ++p)
+			s += tpx_ldf(t.slot(t.rank, par, p) + i);
+		out[i] = s;
 	}
 }
 
@@ -163,64 +233,6 @@ __global__ void argmax_pick_kernel(const float *__restrict__ pairs, int n_pairs,
 	st->n_gen = k + 1;
 	st->token = idx;
 	st->pos = st->pos + 1;
-}
-
-// One-shot exchange over IPC-mapped peer buffers (tensor parallelism without
-// RCCL; works with several ranks on one GPU). Each rank's buffer: two data
-// slots of S floats, 64 arrival flags (written by the peers), a sequence word.
-// Exchange k (seq = k + 1): the producer kernel already left this rank's data
-// in slot seq & 1; signal every peer (system-scope store of seq into its flag
-// [rank]), wait until every peer's flag here reaches seq (bounded), then
-//   SUM:    out[i] = sum over ranks p (in rank order) of slot_p[offset + i]
-//   GATHER: out[p * count + i] = slot_p[offset + i]
-// with system-scope loads. A slot is rewritten two exchanges later, after
-// every peer has signalled the exchange in between, i.e. finished reading it.
-enum { IPC_SUM = 0, IPC_GATHER = 1 };
-__global__ __launch_bounds__(1024) void ipc_exchange_kernel(float *const *__restrict__ bufs, int rank, int n_ranks,
-                                                            int S, int offset, int count, int mode,
-                                                            float *__restrict__ out) {
-	float *const own = bufs[rank];
-	unsigned *const flags = (unsigned *)(own + 2 * (size_t)S);
-	unsigned *const seqp = flags + 64;
-	const unsigned seq = *seqp + 1u; // only this rank's (stream-ordered) kernels write it
-	const size_t so = (size_t)(seq & 1u) * S + offset;
-	if (threadIdx.x == 0) {
-		__builtin_amdgcn_fence(__ATOMIC_RELEASE, ""); // this rank's slot data before the signal
-		for (int p = 0; p < n_ranks; ++p)
-			if (p != rank)
-				__hip_atomic_store((unsigned *)(bufs[p] + 2 * (size_t)S) + rank, seq, __ATOMIC_RELAXED,
-				                   __HIP_MEMORY_SCOPE_SYSTEM);
-		for (int p = 0; p < n_ranks; ++p) {
-			if (p == rank)
-				continue;
-			long spins = 0;
-			while ((int)(__hip_atomic_load(flags + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - seq) < 0) {
-				if (++spins > (1l << 24)) { // a peer never arrived: give up (results wrong, no hang)
-					__hip_atomic_store(flags + 63, 0xdeadu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-					break;
-				}
-				__builtin_amdgcn_s_sleep(2);
-			}
-		}
-		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-	}
-	__syncthreads();
-	if (mode == IPC_SUM) {
-		for (int i = threadIdx.x; i < count; i += blockDim.x) {
-			float s = 0.0f;
-			for (int p = 0; p < n_ranks; ++p)
-				s += __hip_atomic_load(bufs[p] + so + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-			out[i] = s;
-		}
-	} else {
-		for (int p = 0; p < n_ranks; ++p)
-			for (int i = threadIdx.x; i < count; i += blockDim.x)
-				out[(size_t)p * count + i] =
-				    __hip_atomic_load(bufs[p] + so + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-	}
-	__syncthreads();
-	if (threadIdx.x == 0)
-		*seqp = seq;
 }
 
 // Deterministic synthetic initialiser — the same integer hash as the CPU

@@ -148,7 +148,8 @@ struct RowsMode<PQKV<WT>> {
 };
 
 template <class WT, class P, bool NORM, int THREADS, int U>
-static int launch_rb_t(const P &p, const float *x, const float *normw, float eps, int wpc, hipStream_t st) {
+static int launch_rb_t(const P &p, const float *x, const float *normw, float eps, int wpc, hipStream_t st,
+                       const TpX &tin) {
 	const int nb = std::max(1, std::min(p.n_groups, device_cu_count() * std::max(1, wpc)));
 	const int ngl = (p.n_groups + nb - 1) / nb;
 	if constexpr (RowsMode<P>::value) {
@@ -164,7 +165,7 @@ static int launch_rb_t(const P &p, const float *x, const float *normw, float eps
 			    ((size_t)((p.n + 3) & ~3) + 64 + (size_t)ngl * P::R * (THREADS / YALM_WAVE)) * sizeof(float);
 			if (lds > 65536)
 				HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-			hipLaunchKernelGGL(kern, dim3(nb), dim3(THREADS), lds, st, p, x, normw, eps);
+			hipLaunchKernelGGL(kern, dim3(nb), dim3(THREADS), lds, st, p, x, normw, eps, tin);
 			HIPCHK(hipGetLastError());
 			return YALM_OK;
 		}
@@ -173,7 +174,7 @@ static int launch_rb_t(const P &p, const float *x, const float *normw, float eps
 	const size_t lds = ((size_t)((p.n + 3) & ~3) + 64 + (size_t)ngl * P::R * (THREADS / YALM_WAVE)) * sizeof(float);
 	if (lds > 65536)
 		HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-	hipLaunchKernelGGL(kern, dim3(nb), dim3(THREADS), lds, st, p, x, normw, eps);
+	hipLaunchKernelGGL(kern, dim3(nb), dim3(THREADS), lds, st, p, x, normw, eps, tin);
 	HIPCHK(hipGetLastError());
 	return YALM_OK;
 }
@@ -210,37 +211,43 @@ static GemvCfg default_rb_cfg(int kind) {
 }
 
 template <class WT, class P, bool NORM, int THREADS>
-static int launch_rb_u(const P &p, const float *x, const float *normw, float eps, int U, int wpc, hipStream_t st) {
+static int launch_rb_u(const P &p, const float *x, const float *normw, float eps, int U, int wpc, hipStream_t st,
+                       const TpX &tin) {
 	switch (U) {
 	case 2:
-		return launch_rb_t<WT, P, NORM, THREADS, 2>(p, x, normw, eps, wpc, st);
+		return launch_rb_t<WT, P, NORM, THREADS, 2>(p, x, normw, eps, wpc, st, tin);
 	case 8:
-		return launch_rb_t<WT, P, NORM, THREADS, 8>(p, x, normw, eps, wpc, st);
+		return launch_rb_t<WT, P, NORM, THREADS, 8>(p, x, normw, eps, wpc, st, tin);
 	default:
-		return launch_rb_t<WT, P, NORM, THREADS, 4>(p, x, normw, eps, wpc, st);
+		return launch_rb_t<WT, P, NORM, THREADS, 4>(p, x, normw, eps, wpc, st, tin);
 	}
 }
 
 template <class WT, class P, bool NORM>
 static int launch_rb(const P &p, const float *x, const float *normw, float eps, int kind, GemvCfg want,
-                     hipStream_t st) {
+                     hipStream_t st, const TpX &tin) {
 	const GemvCfg def = default_rb_cfg<WT>(kind);
 	const int threads = want.threads ? want.threads : def.threads;
 	const int U = want.U ? want.U : def.U;
 	const int wpc = want.gpw ? want.gpw : def.gpw;
 	if (threads == 256)
-		return launch_rb_u<WT, P, NORM, 256>(p, x, normw, eps, U, wpc, st);
+		return launch_rb_u<WT, P, NORM, 256>(p, x, normw, eps, U, wpc, st, tin);
 	if (threads == 1024)
-		return launch_rb_u<WT, P, NORM, 1024>(p, x, normw, eps, U, wpc, st);
-	return launch_rb_u<WT, P, NORM, 512>(p, x, normw, eps, U, wpc, st);
+		return launch_rb_u<WT, P, NORM, 1024>(p, x, normw, eps, U, wpc, st, tin);
+	return launch_rb_u<WT, P, NORM, 512>(p, x, normw, eps, U, wpc, st, tin);
 }
 
+// tin: the exchange this launch consumes (tensor parallelism over IPC), default none
 template <class WT, class P, bool NORM>
 static int launch_gemv(const P &p, const float *x, const float *normw, float eps, int kind, GemvCfg want,
-                       hipStream_t st) {
+                       hipStream_t st, const TpX &tin = TpX{}) {
 	const size_t lds = (size_t)((p.n + 3) & ~3) * sizeof(float) + 64 * sizeof(float);
 	constexpr int CH = YALM_WAVE * WT::EPL;
 	if (p.n % CH != 0) { // ragged K: generic kernel (tests / unusual shapes)
+		if (tin.n > 0) {
+			set_err("tensor parallel: dim must be a multiple of 64 x elements per 16 bytes");
+			return YALM_ERR_UNSUPPORTED;
+		}
 		auto kern = gemv_kernel<WT, P, 4, NORM>;
 		if (lds > 65536)
 			HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -249,14 +256,15 @@ static int launch_gemv(const P &p, const float *x, const float *normw, float eps
 		HIPCHK(hipGetLastError());
 		return YALM_OK;
 	}
-	return launch_rb<WT, P, NORM>(p, x, normw, eps, kind, want, st);
+	return launch_rb<WT, P, NORM>(p, x, normw, eps, kind, want, st, tin);
 }
 
 // The decoder's weight-streaming GEMVs: gemv_rb_kernel with the geometry set
 // through yalm_set_gemv_config (or the per-kind default).
 template <class WT, class P, bool NORM>
-static int launch_gemv_d(yalm_decoder_s *d, const P &p, const float *x, const float *normw, float eps, int kind) {
-	return launch_gemv<WT, P, NORM>(p, x, normw, eps, kind, d->gemv[kind], d->stream);
+static int launch_gemv_d(yalm_decoder_s *d, const P &p, const float *x, const float *normw, float eps, int kind,
+                         const TpX &tin = TpX{}) {
+	return launch_gemv<WT, P, NORM>(p, x, normw, eps, kind, d->gemv[kind], d->stream, tin);
 }
 
 static bool attn_supported(int head_dim, int G) {
@@ -342,23 +350,27 @@ static int launch_attn(int head_dim, int n_heads, int n_kv, const float *q, cons
 }
 
 // ---- attention + Wo in one launch (attn_wo.h)
-template <class WT, int GT, int XS>
+template <class WT, int GT, int KB>
 static const void *attn_wo_fn() {
-	return (const void *)attn_wo_kernel<WT, GT, XS>;
+	return (const void *)attn_wo_kernel<WT, GT, KB>;
 }
-template <class WT, int XS>
+template <class WT, int KB>
 static const void *attn_wo_fn_g(int G) {
-	return G <= 1 ? attn_wo_fn<WT, 1, XS>() : G <= 2 ? attn_wo_fn<WT, 2, XS>() : G <= 4 ? attn_wo_fn<WT, 4, XS>()
-	                                                                         : attn_wo_fn<WT, 8, XS>();
+	return G <= 1 ? attn_wo_fn<WT, 1, KB>() : G <= 2 ? attn_wo_fn<WT, 2, KB>() : G <= 4 ? attn_wo_fn<WT, 4, KB>()
+	                                                                         : attn_wo_fn<WT, 8, KB>();
 }
-static const void *attn_wo_pick(int dtype, int G, int XS) {
-	if (dtype == YALM_F16)
-		return XS == 1 ? attn_wo_fn_g<WF16, 1>(G) : attn_wo_fn_g<WF16, 2>(G);
-	return XS == 1 ? attn_wo_fn_g<WF8, 1>(G) : attn_wo_fn_g<WF8, 2>(G);
+template <class WT>
+static const void *attn_wo_fn_kb(int G, int KB) {
+	return KB == 1 ? attn_wo_fn_g<WT, 1>(G) : KB == 2 ? attn_wo_fn_g<WT, 2>(G) : KB == 4 ? attn_wo_fn_g<WT, 4>(G)
+	                                                                            : attn_wo_fn_g<WT, 8>(G);
+}
+static const void *attn_wo_pick(int dtype, int G, int KB) {
+	return dtype == YALM_F16 ? attn_wo_fn_kb<WF16>(G, KB) : attn_wo_fn_kb<WF8>(G, KB);
 }
 // The fused launch's plan for a (per-rank) config: 1 with the key splits S and the grid,
 // or 0 = separate attention and Wo launches. Fused needs head_dim 128, G <= 8, fp16 / fp8
-// Wo rows of 4 or 8 KB, and the whole grid (attention, one merger per query head, Wo)
+// Wo rows of 1, 2, 4 or 8 KiB (one GPU: 4 / 8; a tensor-parallel rank's Wo slice: 1 / 2 too),
+// and the whole grid (attention, one merger per query head, Wo)
 // within the co-resident workgroup slots: a workgroup past them is dispatched only when
 // an earlier one exits, and at short contexts every attention workgroup without keys
 // still holds its slot for the kv_len load (S 32 at Mistral: 256 + 32 + 256 = 544 > 512
@@ -377,7 +389,7 @@ extern "C" int yalm_attn_wo_plan(const yalm_config *cp, int slots, int *splits, 
 	if (G < 1 || G > 8 || (c.weight_dtype != YALM_F16 && c.weight_dtype != YALM_F8E5M2))
 		return 0;
 	const int rb = c.n_heads * c.head_dim * (c.weight_dtype == YALM_F16 ? 2 : 1);
-	if ((rb != 4096 && rb != 8192) || c.dim < AWO_RPW)
+	if ((rb != 1024 && rb != 2048 && rb != 4096 && rb != 8192) || c.dim < AWO_RPW)
 		return 0;
 	const int nchunks = (c.max_seq_len + attn_chunk<128>() - 1) / attn_chunk<128>();
 	const int n_wo = (c.dim + AWO_RPW - 1) / AWO_RPW;
@@ -394,25 +406,28 @@ extern "C" int yalm_attn_wo_plan(const yalm_config *cp, int slots, int *splits, 
 	return 1;
 }
 
-// Single-GPU decoders whose plan (yalm_attn_wo_plan) fuses.
+// Decoders whose plan (yalm_attn_wo_plan, on the per-rank config) fuses: one GPU, and
+// (round 5) every tensor-parallel rank too -- the Wo workgroups then write the rank's
+// partial for the all-reduce (RCCL) or push it to the exchange (IPC, tp_exchange.h).
 static int attn_wo_init(yalm_decoder_s *d) {
 	const yalm_config &c = d->c;
 	const char *env = getenv("YALM_ATTN_WO");
 	if (env && atoi(env) == 0)
 		return YALM_OK;
-	if (d->comm || d->ipc || d->tp_size > 1 || c.head_dim != 128)
+	if (c.head_dim != 128)
 		return YALM_OK;
 	const int G = c.n_heads / c.n_kv_heads;
 	const int rb = c.n_heads * c.head_dim * (c.weight_dtype == YALM_F16 ? 2 : 1);
 	if (!yalm_attn_wo_plan(&c, 1 << 30, nullptr, nullptr))
 		return YALM_OK;
 	int occ = 0; // the Wo workgroups spin, but only on attention workgroups dispatched before them
-	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, attn_wo_pick(c.weight_dtype, G, rb / 4096), ATTN_THREADS,
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, attn_wo_pick(c.weight_dtype, G, rb / 1024), ATTN_THREADS,
 	                                                 0) != hipSuccess ||
 	    occ < 1)
 		return YALM_OK;
 	if (!yalm_attn_wo_plan(&c, occ * device_cu_count(), &d->awo_S, &d->awo_nb))
 		return YALM_OK;
+	d->awo_slots = occ * device_cu_count();
 	// per layer: the attention output as {value, epoch} granules (zero tags never match:
 	// the epoch is >= 1 from the first forward / yalm_block on)
 	const size_t gran = (size_t)c.n_layers * c.n_heads * c.head_dim;
@@ -456,8 +471,8 @@ int awo_check(yalm_decoder_s *d) {
 			return YALM_ERR_HIP;
 		}
 	}
-	if (d->ipc) {
-		unsigned *flag = (unsigned *)(d->ipc_own + 2 * (size_t)d->ipc_S) + 63;
+	if (d->ipc) { // tp_exchange.h: a consumer's bounded wait for a peer's exchange gave up
+		unsigned *flag = (unsigned *)(d->ipc_own + 2 * (size_t)d->tp_size * d->ipc_S) + 65;
 		unsigned e = 0;
 		HIPCHK(hipMemcpy(&e, flag, sizeof(e), hipMemcpyDeviceToHost));
 		if (e) {
@@ -469,21 +484,24 @@ int awo_check(yalm_decoder_s *d) {
 	return YALM_OK;
 }
 
-template <class WT, int GT, int XS>
+template <class WT, int GT, int KB>
 static void launch_attn_wo_k(yalm_decoder_s *d, const yalm_block_weights &w, const AttnWoArgs &p) {
-	attn_wo_kernel<WT, GT, XS><<<d->awo_nb, ATTN_THREADS, 0, d->stream>>>(d->q, w.key_cache, w.value_cache, d->step, p);
+	attn_wo_kernel<WT, GT, KB><<<d->awo_nb, ATTN_THREADS, 0, d->stream>>>(d->q, w.key_cache, w.value_cache, d->step, p);
 }
-template <class WT, int XS>
+template <class WT, int KB>
 static void launch_attn_wo_g(yalm_decoder_s *d, const yalm_block_weights &w, const AttnWoArgs &p, int G) {
 	if (G <= 1)
-		launch_attn_wo_k<WT, 1, XS>(d, w, p);
+		launch_attn_wo_k<WT, 1, KB>(d, w, p);
 	else if (G <= 2)
-		launch_attn_wo_k<WT, 2, XS>(d, w, p);
+		launch_attn_wo_k<WT, 2, KB>(d, w, p);
 	else if (G <= 4)
-		launch_attn_wo_k<WT, 4, XS>(d, w, p);
+		launch_attn_wo_k<WT, 4, KB>(d, w, p);
 	else
-		launch_attn_wo_k<WT, 8, XS>(d, w, p);
+		launch_attn_wo_k<WT, 8, KB>(d, w, p);
 }
+// The fused attention + Wo launch of one layer. One GPU: x += Wo attn(q). Tensor parallel:
+// the rank's partial (+ x on rank 0) -- into xs, then the RCCL all-reduce into x; or pushed
+// to the IPC exchange (consumed by the GLU GEMV's x staging, tp_exchange.h).
 template <class WT>
 static int launch_attn_wo(yalm_decoder_s *d, const yalm_block_weights &w, int layer) {
 	const yalm_config &c = d->c;
@@ -502,30 +520,42 @@ static int launch_attn_wo(yalm_decoder_s *d, const yalm_block_weights &w, int la
 	p.gran = d->awo_gran + (size_t)layer * p.q_dim;
 	p.wo = (const char *)w.wo;
 	p.x = d->x;
+	p.out = d->comm ? d->xs : d->x;
+	p.add_base = d->tp_rank == 0;
+	p.push = d->ipc ? d->tpx : TpX{};
 	p.err = d->awo_err;
 	p.trace = d->awo_trace;
 	p.delay = d->awo_delay;
 	const int G = c.n_heads / c.n_kv_heads;
 	if constexpr (WT::BYTES == 2 || WT::BYTES == 1) {
-		if (p.q_dim * WT::BYTES == 4096)
+		switch (p.q_dim * WT::BYTES) {
+		case 1024:
 			launch_attn_wo_g<WT, 1>(d, w, p, G);
-		else
+			break;
+		case 2048:
 			launch_attn_wo_g<WT, 2>(d, w, p, G);
+			break;
+		case 4096:
+			launch_attn_wo_g<WT, 4>(d, w, p, G);
+			break;
+		default:
+			launch_attn_wo_g<WT, 8>(d, w, p, G);
+		}
 	}
 	HIPCHK(hipGetLastError());
+	if (d->comm && ncclAllReduce(d->xs, d->x, c.dim, ncclFloat, ncclSum, (ncclComm_t)d->comm, d->stream) != ncclSuccess) {
+		set_err("ncclAllReduce failed");
+		return YALM_ERR_HIP;
+	}
 	return YALM_OK;
 }
 
-static const unsigned *ipc_seq(const yalm_decoder_s *d) {
-	return (const unsigned *)(d->ipc_own + 2 * (size_t)d->ipc_S) + 64;
-}
-
-// One tensor-parallel exchange of x alone (the all-reduce that follows the Wo / W2
-// partials): timing hook for the per-token communication cost (yalm_time_kernel id 6).
+// One tensor-parallel exchange of x alone, as a launch of its own: timing hook for the
+// communication cost (yalm_time_kernel id 6). RCCL: one all-reduce. IPC: the consumer side
+// (wait for every rank + sum into x) -- in the forward it runs inside the next GEMV.
 static int enqueue_exchange(yalm_decoder_s *d) {
 	if (d->ipc) {
-		ipc_exchange_kernel<<<1, 1024, 0, d->stream>>>(d->ipc_bufs, d->tp_rank, d->tp_size, d->ipc_S, 0, d->c.dim,
-		                                              IPC_SUM, d->xs);
+		tpx_collect_kernel<<<1, 1024, 0, d->stream>>>(d->tpx, d->c.dim, 0, d->x);
 		HIPCHK(hipGetLastError());
 		return YALM_OK;
 	}
@@ -541,28 +571,23 @@ static int enqueue_exchange(yalm_decoder_s *d) {
 }
 
 // x += W v (fused_matmul_add_residuals). Under tensor parallelism W holds this
-// rank's input columns: rank 0 writes xs = x + W v, the others xs = W v, and
-// one RCCL all-reduce (sum, captured in the graph) lands x + sum_r W_r v_r in x
-// on every rank (identical bits on all ranks).
+// rank's input columns: rank 0's partial carries x. RCCL: rank 0 writes xs = x + W v, the
+// others xs = W v, and one all-reduce (sum, captured in the graph) lands the sum in x on
+// every rank (identical bits). IPC: the partial is pushed to every rank's exchange slot
+// (PPush, tp_exchange.h); the next GEMV sums the slots while its weights stream in.
 template <class WT>
 static int enqueue_residual_gemv(yalm_decoder_s *d, const void *W, int n, const float *v, int kind) {
 	const yalm_config &c = d->c;
 	hipStream_t st = d->stream;
-	if (d->ipc) { // partial (+ x on rank 0) into this exchange's slot, then SUM over the ranks into x
-		PSlot<WT, 1> p;
+	if (d->ipc) {
+		PPush<WT, 1> p;
 		p.W = (const char *)W;
 		p.n = n;
-		p.slots = d->ipc_own;
-		p.S = d->ipc_S;
-		p.offset = 0;
-		p.seq = ipc_seq(d);
 		p.base = d->tp_rank == 0 ? d->x : nullptr;
+		p.t = d->tpx;
+		p.offset = 0;
 		p.n_groups = c.dim;
-		TRY((launch_gemv<WT, PSlot<WT, 1>, false>(p, v, nullptr, 0.f, kind, d->gemv[kind], st)));
-		ipc_exchange_kernel<<<1, 1024, 0, st>>>(d->ipc_bufs, d->tp_rank, d->tp_size, d->ipc_S, 0, c.dim, IPC_SUM,
-		                                       d->x);
-		HIPCHK(hipGetLastError());
-		return YALM_OK;
+		return launch_gemv<WT, PPush<WT, 1>, false>(p, v, nullptr, 0.f, kind, d->gemv[kind], st);
 	}
 	if (!d->comm) {
 		PResidual<WT, 1> p;
@@ -595,12 +620,27 @@ static int enqueue_residual_gemv(yalm_decoder_s *d, const void *W, int n, const 
 	return YALM_OK;
 }
 
+// The exchange descriptor for a consumer launch. When this rank shares its GPU with a peer
+// (tests: several rank processes on one device), a 1-wave gate launch waits for the exchange
+// first: a consumer whose 256 workgroups spin in tpx_wait could otherwise hold every CU a
+// peer's producer needs (a deadlock the bounded wait only reports). One GPU per rank (the
+// real configuration) needs no gate: the consumer waits inside its own launch.
+static TpX tpx_consume(yalm_decoder_s *d) {
+	if (d->tpx_gate)
+		tpx_gate_kernel<<<1, 64, 0, d->stream>>>(d->tpx);
+	return d->tpx;
+}
+
+// One layer. x_exchanged: the layer's input x is the previous layer's W2 exchange (IPC
+// tensor parallelism: the QKV GEMV consumes it), not a local x (the embedding of layer 0,
+// or the x yalm_block / yalm_set_x left).
 template <class WT>
-static int enqueue_layer_t(yalm_decoder_s *d, int l) {
+static int enqueue_layer_t(yalm_decoder_s *d, int l, bool x_exchanged) {
 	const yalm_config &c = d->c;
 	const yalm_block_weights &w = d->b[l];
 	hipStream_t st = d->stream;
 	const int q_dim = c.n_heads * c.head_dim, kv_dim = c.n_kv_heads * c.head_dim;
+	const TpX none{};
 	{
 		PQKV<WT> p;
 		p.wq = (const char *)w.wq;
@@ -617,7 +657,8 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 		p.q_out = d->q;
 		p.kcache = w.key_cache;
 		p.vcache = w.value_cache;
-		TRY((launch_gemv_d<WT, PQKV<WT>, true>(d, p, d->x, w.rms_att, c.norm_eps, GK_QKV)));
+		TRY((launch_gemv_d<WT, PQKV<WT>, true>(d, p, d->x, w.rms_att, c.norm_eps, GK_QKV,
+		                                         d->ipc && x_exchanged ? tpx_consume(d) : none)));
 	}
 	if (d->attn_wo && WT::BYTES <= 2) {
 		TRY(launch_attn_wo<WT>(d, w, l));
@@ -626,6 +667,7 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 		                d->part, l, c.n_layers, d->awo_err, nullptr, d->xb2, st));
 		TRY(enqueue_residual_gemv<WT>(d, w.wo, q_dim, d->xb2, GK_WO));
 	}
+	// the GLU consumes the Wo exchange under IPC tensor parallelism
 	if (c.act == YALM_SILU) {
 		PGlu<WT, 1> p;
 		p.w1 = (const char *)w.w1;
@@ -633,7 +675,7 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 		p.n = c.dim;
 		p.out = d->hb;
 		p.n_groups = c.hidden_dim;
-		TRY((launch_gemv_d<WT, PGlu<WT, 1>, true>(d, p, d->x, w.rms_ffn, c.norm_eps, GK_GLU)));
+		TRY((launch_gemv_d<WT, PGlu<WT, 1>, true>(d, p, d->x, w.rms_ffn, c.norm_eps, GK_GLU, d->ipc ? tpx_consume(d) : none)));
 	} else {
 		PGlu<WT, 0> p;
 		p.w1 = (const char *)w.w1;
@@ -641,26 +683,28 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l) {
 		p.n = c.dim;
 		p.out = d->hb;
 		p.n_groups = c.hidden_dim;
-		TRY((launch_gemv_d<WT, PGlu<WT, 0>, true>(d, p, d->x, w.rms_ffn, c.norm_eps, GK_GLU)));
+		TRY((launch_gemv_d<WT, PGlu<WT, 0>, true>(d, p, d->x, w.rms_ffn, c.norm_eps, GK_GLU, d->ipc ? tpx_consume(d) : none)));
 	}
 	return enqueue_residual_gemv<WT>(d, w.w2, c.hidden_dim, d->hb, GK_W2);
 }
 
+// Final norm + classifier rows of this rank. IPC tensor parallelism: consume = the GEMV
+// consumes the last layer's W2 exchange; push (OUTPUT_LOGITS) = it also produces the logits
+// gather, this rank's vocabulary rows pushed to every rank's slot.
 template <class WT>
-static int enqueue_logits_t(yalm_decoder_s *d) {
+static int enqueue_logits_t(yalm_decoder_s *d, bool consume, bool push) {
 	const yalm_config &c = d->c;
-	if (d->ipc) { // this rank's vocabulary rows into the exchange slot, after the 2-float argmax pair
-		PSlot<WT, 1> p;
+	const TpX tin = consume ? tpx_consume(d) : TpX{};
+	if (push) {
+		PPush<WT, 1> p;
 		p.W = (const char *)d->wcls;
 		p.n = c.dim;
-		p.slots = d->ipc_own;
-		p.S = d->ipc_S;
-		p.offset = 2;
-		p.seq = ipc_seq(d);
 		p.base = nullptr;
+		p.t = d->tpx;
+		p.offset = 0;
 		p.n_groups = c.vocab_size;
-		return launch_gemv<WT, PSlot<WT, 1>, true>(p, d->x, d->rms_final, c.norm_eps, GK_CLS, d->gemv[GK_CLS],
-		                                           d->stream);
+		return launch_gemv<WT, PPush<WT, 1>, true>(p, d->x, d->rms_final, c.norm_eps, GK_CLS, d->gemv[GK_CLS],
+		                                           d->stream, tin);
 	}
 	if (c.vocab_size % 2 == 0) {
 		PStore<WT, 2> p;
@@ -668,14 +712,14 @@ static int enqueue_logits_t(yalm_decoder_s *d) {
 		p.n = c.dim;
 		p.out = d->logits_local;
 		p.n_groups = c.vocab_size / 2;
-		return launch_gemv_d<WT, PStore<WT, 2>, true>(d, p, d->x, d->rms_final, c.norm_eps, GK_CLS);
+		return launch_gemv_d<WT, PStore<WT, 2>, true>(d, p, d->x, d->rms_final, c.norm_eps, GK_CLS, tin);
 	}
 	PStore<WT, 1> p;
 	p.W = (const char *)d->wcls;
 	p.n = c.dim;
 	p.out = d->logits_local;
 	p.n_groups = c.vocab_size;
-	return launch_gemv_d<WT, PStore<WT, 1>, true>(d, p, d->x, d->rms_final, c.norm_eps, GK_CLS);
+	return launch_gemv_d<WT, PStore<WT, 1>, true>(d, p, d->x, d->rms_final, c.norm_eps, GK_CLS, tin);
 }
 
 template <class WT>
@@ -693,26 +737,19 @@ static int enqueue_begin_t(yalm_decoder_s *d) {
 static int enqueue_forward(yalm_decoder_s *d, int which) {
 	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_begin_t, d));
 	for (int l = 0; l < d->c.n_layers; ++l)
-		TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_layer_t, d, l));
+		TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_layer_t, d, l, l > 0));
 	if (which == GRAPH_HYDRATE)
 		return YALM_OK;
-	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_logits_t, d));
-	if (d->ipc) {
-		if (which == GRAPH_LOGITS) {
-			ipc_exchange_kernel<<<1, 1024, 0, d->stream>>>(d->ipc_bufs, d->tp_rank, d->tp_size, d->ipc_S, 2,
-			                                              d->c.vocab_size, IPC_GATHER, d->logits);
+	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_logits_t, d, d->ipc, d->ipc && which == GRAPH_LOGITS));
+	if (d->ipc) { // tp_exchange.h: no exchange launches
+		if (which == GRAPH_LOGITS) { // every rank's vocabulary slice, side by side
+			tpx_collect_kernel<<<1, 1024, 0, d->stream>>>(d->tpx, d->c.vocab_size, 1, d->logits);
 			HIPCHK(hipGetLastError());
 			HIPCHK(hipMemcpyAsync(d->logits_pinned, d->logits, sizeof(float) * d->vocab_full, hipMemcpyDeviceToHost,
 			                      d->stream));
-		} else {
-			argmax_kernel<<<1, 1024, 0, d->stream>>>(d->ipc_own + 2, d->c.vocab_size, d->step, d->tokens,
-			                                         d->tokens_cap, d->ipc_own, d->tp_rank * d->c.vocab_size,
-			                                         ipc_seq(d), d->ipc_S);
-			HIPCHK(hipGetLastError());
-			ipc_exchange_kernel<<<1, 1024, 0, d->stream>>>(d->ipc_bufs, d->tp_rank, d->tp_size, d->ipc_S, 0, 2,
-			                                              IPC_GATHER, d->amax_all);
-			HIPCHK(hipGetLastError());
-			argmax_pick_kernel<<<1, 1, 0, d->stream>>>(d->amax_all, d->tp_size, d->step, d->tokens, d->tokens_cap);
+		} else { // local first max, pushed; every rank's pair gathered and picked in the same launch
+			argmax_tp_kernel<<<1, 1024, 0, d->stream>>>(d->logits_local, d->c.vocab_size, d->step, d->tokens,
+			                                            d->tokens_cap, d->tpx);
 			HIPCHK(hipGetLastError());
 		}
 		return YALM_OK;
@@ -939,9 +976,13 @@ static int tp_local_config(const yalm_config &f, int tp_size, yalm_config &lc) {
 	return YALM_OK;
 }
 
+// floats per (parity, source rank) slot of the IPC exchange: x, or a rank's vocabulary rows
 static int ipc_slot_floats(const yalm_config &f, int tp_size) {
 	const int need = std::max(f.dim, f.vocab_size / tp_size + 2);
 	return (need + 63) / 64 * 64;
+}
+static size_t ipc_buf_bytes(const yalm_config &f, int tp_size) {
+	return (2 * (size_t)tp_size * ipc_slot_floats(f, tp_size) + TPX_CTRL_WORDS) * sizeof(float);
 }
 
 extern "C" int yalm_tp_unique_id(void *id_out) {
@@ -976,9 +1017,10 @@ extern "C" int yalm_decoder_create_tp(const yalm_config *config, const yalm_mode
 }
 
 extern "C" int yalm_tp_ipc_alloc(const yalm_config *config, int tp_size, void **buf, void *handle_out) {
-	ARGCHK(config && buf && handle_out && tp_size >= 1 && tp_size <= 63, "yalm_tp_ipc_alloc: bad argument");
-	const size_t bytes = (2 * (size_t)ipc_slot_floats(*config, tp_size) + 128) * sizeof(float);
-	HIPCHK(hipMalloc(buf, bytes));
+	ARGCHK(config && buf && handle_out && tp_size >= 1 && tp_size <= 8, "yalm_tp_ipc_alloc: bad argument (1..8 ranks)");
+	const size_t bytes = ipc_buf_bytes(*config, tp_size);
+	// uncached (tp_exchange.h): peers push into it, so no reader's L2 may hold a stale line
+	HIPCHK(hipExtMallocWithFlags(buf, bytes, hipDeviceMallocUncached));
 	HIPCHK(hipMemset(*buf, 0, bytes));
 	hipIpcMemHandle_t h;
 	HIPCHK(hipIpcGetMemHandle(&h, *buf));
@@ -991,9 +1033,11 @@ extern "C" int yalm_decoder_create_tp_ipc(const yalm_config *config, const yalm_
                                           int tp_size, void *own_buf, const void *handles, yalm_stream s,
                                           yalm_decoder *out) {
 	ARGCHK(config && weights && own_buf && handles && out, "yalm_decoder_create_tp_ipc: null argument");
-	ARGCHK(tp_size >= 1 && tp_size <= 63 && tp_rank >= 0 && tp_rank < tp_size, "bad rank / size");
+	ARGCHK(tp_size >= 1 && tp_size <= 8 && tp_rank >= 0 && tp_rank < tp_size, "bad rank / size (1..8 ranks)");
 	yalm_config lc;
 	TRY(tp_local_config(*config, tp_size, lc));
+	ARGCHK(config->dim % (64 * (config->weight_dtype == YALM_F32 ? 4 : config->weight_dtype == YALM_F16 ? 8 : 16)) == 0,
+	       "tensor parallel (IPC): dim must be a multiple of 64 x the elements of a 16-byte load");
 	std::vector<float *> bases(tp_size);
 	std::vector<void *> opened;
 	for (int p = 0; p < tp_size; ++p) {
@@ -1033,6 +1077,26 @@ extern "C" int yalm_decoder_create_tp_ipc(const yalm_config *config, const yalm_
 		return YALM_ERR_HIP;
 	}
 	d->ipc_bufs = (float **)dev_bases;
+	int dev = 0;
+	HIPCHK(hipGetDevice(&dev));
+	for (int p = 0; p < tp_size; ++p) { // a peer's buffer on this device: ranks share the GPU
+		hipPointerAttribute_t at;
+		if (p != tp_rank && hipPointerGetAttributes(&at, bases[p]) == hipSuccess && at.device == dev)
+			d->tpx_gate = true;
+	}
+	// The fused attention + Wo launch's Wo workgroups spin on attention workgroups of the
+	// same launch, which is deadlock-free while the grid is co-resident. Ranks sharing one
+	// GPU launch their grids concurrently; when they cannot all be resident at once, a
+	// workgroup dispatched on a full XCD can trail Wo workgroups already spinning on other
+	// XCDs (measured: TP8 at Mistral dims, 8 processes on one MI355X, the Wo gather timed
+	// out). Those ranks keep the separate attention and Wo launches.
+	if (d->tpx_gate && d->attn_wo && d->awo_nb * tp_size > d->awo_slots)
+		d->attn_wo = false;
+	d->tpx.bufs = d->ipc_bufs;
+	d->tpx.rank = tp_rank;
+	d->tpx.n = tp_size;
+	d->tpx.S = d->ipc_S;
+	d->tpx.xw = d->x;
 	return YALM_OK;
 }
 
@@ -1138,7 +1202,11 @@ extern "C" int yalm_block(yalm_decoder d, int layer, int pos, int kv_sink, int k
 	       "bad kv indices");
 	set_step_full_kernel<<<1, 1, 0, d->stream>>>(d->step, pos, kv_sink, kv_pos, kv_len);
 	HIPCHK(hipGetLastError());
-	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_layer_t, d, layer));
+	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_layer_t, d, layer, false));
+	if (d->ipc) { // the layer's W2 pushed its partial: collect the sum into x (a forward's next GEMV would)
+		tpx_collect_kernel<<<1, 1024, 0, d->stream>>>(d->tpx, d->c.dim, 0, d->x);
+		HIPCHK(hipGetLastError());
+	}
 	HIPCHK(hipStreamSynchronize(d->stream));
 	return awo_check(d);
 }
@@ -1213,8 +1281,8 @@ static int enqueue_one_t(yalm_decoder_s *d, int kernel_id, int l) {
 	case 1:
 		return launch_attn(c.head_dim, c.n_heads, c.n_kv_heads, d->q, w.key_cache, w.value_cache, d->step,
 		                   c.max_seq_len, d->part, l, c.n_layers, d->awo_err, nullptr, d->xb2, d->stream);
-	case 5:
-		return enqueue_logits_t<WT>(d);
+	case 5: // (local x: the timing hooks never take part in an exchange, except kernels 6 and 8)
+		return enqueue_logits_t<WT>(d, false, false);
 	case 6:
 		return enqueue_exchange(d);
 	case 8: // fused attention + Wo
@@ -1224,6 +1292,27 @@ static int enqueue_one_t(yalm_decoder_s *d, int kernel_id, int l) {
 	}
 	set_err("bad kernel_id");
 	return YALM_ERR_ARG;
+}
+
+extern "C" int yalm_graph_kernels(yalm_decoder d, int mode, int *kernels, int *nodes) {
+	ARGCHK(d && kernels && mode >= 0 && mode < N_GRAPHS, "yalm_graph_kernels: bad argument");
+	ARGCHK(!d->eager, "yalm_graph_kernels: the decoder launches eagerly (YALM_EAGER)");
+	TRY(ensure_graph(d, mode));
+	size_t n = 0;
+	HIPCHK(hipGraphGetNodes(d->graph[mode], nullptr, &n));
+	std::vector<hipGraphNode_t> v(n);
+	if (n)
+		HIPCHK(hipGraphGetNodes(d->graph[mode], v.data(), &n));
+	int k = 0;
+	for (auto node : v) {
+		hipGraphNodeType t;
+		HIPCHK(hipGraphNodeGetType(node, &t));
+		k += t == hipGraphNodeTypeKernel;
+	}
+	*kernels = k;
+	if (nodes)
+		*nodes = (int)n;
+	return YALM_OK;
 }
 
 extern "C" int yalm_decoder_attn_wo(yalm_decoder d) {
@@ -1327,7 +1416,7 @@ extern "C" const char *yalm_kernel_name(yalm_decoder d, int kernel_id) {
 		s = gk + ", PStore<";
 		break;
 	case 6:
-		s = d->ipc ? "ipc_exchange_kernel" : d->comm ? "AllReduce" : "";
+		s = d->ipc ? "tpx_collect_kernel" : d->comm ? "AllReduce" : "";
 		break;
 	case 8:
 		s = std::string("attn_wo_kernel<") + wt + ", ";

@@ -49,6 +49,14 @@ static bool print_token_ids() {
 	return e && atoi(e) != 0;
 }
 
+// The sampler's seed: the clock, as the reference (main.cpp constructs Sampler(config,
+// get_timestamp_ms())); YALM_SEED fixes it for reproducible runs (tests: the passkey
+// value and position come from std::rand after Sampler's srand).
+static uint64_t sampler_seed() {
+	const char *e = getenv("YALM_SEED");
+	return e ? strtoull(e, nullptr, 10) : now_ms();
+}
+
 static void setup_device(const std::string &device, Model &model, InferenceState &state) {
 	if (device == "cpu") {
 		fprintf(stderr, "error: -d cpu is the reference's own CPU backend (src/infer.cpp); this engine implements "
@@ -80,7 +88,7 @@ static void run_completion(const std::string &path, const std::string &device, c
 	}
 	Model model(data, context);
 	InferenceState state(model.config);
-	Sampler sampler(model.config, now_ms());
+	Sampler sampler(model.config, sampler_seed());
 	Tokenizer tokenizer(data);
 	std::cout << "Model active bytes with full context window: " << model.config->active_bytes(model.config->max_seq_len)
 	          << std::endl;
@@ -150,7 +158,7 @@ static void run_perplexity(const std::string &path, const std::string &device, c
 	}
 	Model model(data, context);
 	InferenceState state(model.config);
-	Sampler sampler(model.config, now_ms());
+	Sampler sampler(model.config, sampler_seed());
 	Tokenizer tokenizer(data);
 	std::cout << "Model active bytes with full context window: " << model.config->active_bytes(model.config->max_seq_len)
 	          << std::endl;
@@ -202,7 +210,7 @@ static void run_passkey(const std::string &path, const std::string &device, int 
 	}
 	Model model(data, context);
 	InferenceState state(model.config);
-	Sampler sampler(model.config, now_ms());
+	Sampler sampler(model.config, sampler_seed());
 	Tokenizer tokenizer(data);
 	std::cout << "Model active bytes with full context window: " << model.config->active_bytes(model.config->max_seq_len)
 	          << std::endl;
@@ -225,21 +233,33 @@ static void run_passkey(const std::string &path, const std::string &device, int 
 	printf("Passkey test:\n  prompt: %zu tokens\n  passkey: %d\n  passkey token index: ~%d\n\n", encoding.size(),
 	       passkey, (int)(((float)ppos) / n_junk * encoding.size()));
 	const size_t N = encoding.size();
-	for (size_t pos = 0; pos < N; ++pos) {
+	// the positions inside the context window before the last one in one batched prefill
+	// (yalm_prefill; the reference hydrates them one forward each, main.cpp:228-232); the
+	// rest -- past max_seq_len (sliding window + sinks) and the last prompt token, whose
+	// logits start the answer -- one forward each
+	size_t first = 0;
+	const size_t H = std::min(N - 1, (size_t)model.config->max_seq_len);
+	if (H >= 3 && model.prefill(state, encoding.data(), (int)H, 0, nullptr))
+		first = H;
+	for (size_t pos = first; pos < N; ++pos) {
 		std::cout << "\r Running passkey test..." << pos + 1 << "/" << N << std::flush;
 		model.forward(state, encoding[pos], (int)pos,
 		              pos + 1 == N ? InferenceMode::OUTPUT_LOGITS : InferenceMode::HYDRATE_KV_CACHE);
 	}
 	std::cout << std::endl << SUFFIX << std::flush;
+	std::string ids;
 	for (size_t pos = N; pos < N + 16; ++pos) {
 		const int token = sampler.sample_argmax(state);
 		std::cout << tokenizer.decode_one(encoding.back(), token) << std::flush;
+		ids += std::to_string(token) + " ";
 		encoding.push_back(token);
 		if (token == tokenizer.eos_id || token == tokenizer.eot_id)
 			break;
 		model.forward(state, token, (int)pos);
 	}
 	std::cout << std::endl;
+	if (print_token_ids())
+		fprintf(stderr, "TOKENS: %s\n", ids.c_str());
 }
 
 int main(int argc, char *argv[]) {

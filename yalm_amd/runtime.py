@@ -125,6 +125,7 @@ _sig("yalm_prefill_time", c_int, [c_void_p, c_int, c_int, ctypes.POINTER(c_float
 _sig("yalm_gemm_f16", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int])
 _sig("yalm_attn_prefill", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int])
 _sig("yalm_set_prefill_forms", c_int, [c_void_p, ctypes.c_char_p])
+_sig("yalm_graph_kernels", c_int, [c_void_p, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)])
 _sig("yalm_attn_wo_plan", c_int, [c_void_p, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)])
 
 EXPORTED = [
@@ -136,7 +137,7 @@ EXPORTED = [
     "yalm_prefill", "yalm_prefill_time", "yalm_gemm_f16", "yalm_attn_prefill", "yalm_tp_unique_id",
     "yalm_decoder_create_tp", "yalm_copy_2d", "yalm_tp_ipc_alloc", "yalm_decoder_create_tp_ipc",
     "yalm_decoder_attn_wo", "yalm_attn_wo_trace", "yalm_stream_envelope",
-    "yalm_argmax", "yalm_set_prefill_forms", "yalm_attn_wo_plan",
+    "yalm_argmax", "yalm_set_prefill_forms", "yalm_attn_wo_plan", "yalm_graph_kernels",
 ]
 
 HYDRATE_KV_CACHE, OUTPUT_LOGITS = 0, 1
@@ -487,6 +488,12 @@ class Decoder:
         nb, na = c_int(), c_int()
         check(lib.yalm_attn_wo_trace(self.h, buf.ctypes.data, buf.size, ctypes.byref(nb), ctypes.byref(na)))
         return buf[: 16 * nb.value].reshape(nb.value, 16), na.value
+
+    def graph_kernels(self, mode: int = 2) -> int:
+        """Kernel launches per forward of graph `mode` (2 = the device greedy step)."""
+        k, n = c_int(), c_int()
+        check(lib.yalm_graph_kernels(self.h, mode, ctypes.byref(k), ctypes.byref(n)))
+        return k.value
 
     def kernel_name(self, kernel_id: int) -> str:
         return lib.yalm_kernel_name(self.h, kernel_id).decode()
