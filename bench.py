@@ -478,6 +478,11 @@ def main():
             sys.exit("bench.py --gpus N under a profiler: start the ranks with a launcher outside it "
                      "(python -m torch.distributed.run ... bench.py) and put rocprofv3 on each rank's program")
         sys.exit(spawn_ranks(args.gpus))
+    # stdout carries exactly one JSON line: whatever the libraries print there (RCCL's version
+    # banner at communicator creation, HIP runtime notes) goes to stderr instead
+    sys.stdout.flush()
+    real_stdout = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -530,7 +535,7 @@ def main():
     tp_size = world if tp else 1
     if args.long_only:
         print(json.dumps(long_context_leg(runtime, M, cfg, dm, steps=args.long_steps,
-                                          kernel_iters=args.kernel_iters)), flush=True)
+                                          kernel_iters=args.kernel_iters)), file=real_stdout, flush=True)
         dec.close()
         dm.close()
         return
@@ -724,7 +729,7 @@ def main():
             except Exception as e:  # report, never hide
                 out["prefill"]["cpu_baseline"] = {"error": repr(e)[:300]}
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=real_stdout, flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

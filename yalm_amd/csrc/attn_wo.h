@@ -236,7 +236,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 	// writes x): the read-modify-write at the end costs no load round trip
 	const float xres = p.add_base ? p.x[lrow0 + (tid & (AWO_RPW - 1))] : 0.0f;
 	const bool push = p.push.n > 0;
-	const unsigned par = push ? tpx_seq(p.push) & 1u : 0u; // exchange parity, read ahead of the stream
+	const unsigned xg = push ? p.push.g() : 0u; // exchange index, read ahead of the stream
 	if (p.delay > 0) {
 		const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 		while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)p.delay)
@@ -307,12 +307,10 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 		const float s = KB >= 4 ? (rowpart[tid][0] + rowpart[tid][1]) + (rowpart[tid][2] + rowpart[tid][3])
 		                        : (RPL == 4 ? rowpart[tid][0] : rowpart[tid][0] + rowpart[tid][1]);
 		if (push)
-			tpx_put(p.push, par, row, xres + s);
+			tpx_put(p.push, xg, row, xres + s);
 		else
 			p.out[row] = xres + s;
 	}
-	if (push) // this launch's Wo workgroups produce the exchange: the last one bumps the counts
-		tpx_arrive(p.push, (p.dim + AWO_RPW - 1) / AWO_RPW);
 	if (tr) {
 		tr[3] = __builtin_amdgcn_s_memrealtime(), tr[11] = __builtin_amdgcn_s_memtime();
 		tr[0] = t_start, tr[8] = c_start, tr[1] = t_slice, tr[9] = c_slice, tr[2] = t_poll, tr[10] = c_poll;

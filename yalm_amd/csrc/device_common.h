@@ -25,7 +25,8 @@ struct StepState {
 	int n_gen;   // number of greedy tokens produced so far (device loop)
 	unsigned epoch; // launch generation: +1 per forward (step_begin_kernel) and per test-hook block
 	                // (set_step_full_kernel); in-launch hand-off flags carry it, so they never need a reset
-	int pad;
+	unsigned xbase; // IPC tensor parallelism (tp_exchange.h): this launch sequence's first exchange index
+	unsigned xnext; // the next sequence's (xbase + the exchanges this one uses)
 };
 
 // Cross-lane exchange without the LDS crossbar: __shfl_xor lowers to

@@ -111,8 +111,8 @@ struct PAddTo {
 };
 
 // IPC tensor-parallel producer (tp_exchange.h): row value (+ the residual base on rank 0)
-// pushed into this rank's slot of every rank's exchange buffer, at element offset + row;
-// the launch's last workgroup then bumps this rank's exchange count everywhere (tail).
+// pushed into this rank's slot of every rank's exchange buffer, at element offset + row, as
+// {value, tag} granules: no tail, no counter (the granule is its own ready flag).
 template <class WT, int R_>
 struct PPush {
 	static constexpr int R = R_;
@@ -122,8 +122,8 @@ struct PPush {
 	TpX t;
 	int offset;
 	int n_groups;
-	mutable unsigned par = 0; // parity of this exchange (read in prologue, ahead of the stream's end)
-	__device__ __forceinline__ void prologue() const { par = tpx_seq(t) & 1u; }
+	mutable unsigned xg = 0; // this launch's exchange index (read in prologue, ahead of the stream's end)
+	__device__ __forceinline__ void prologue() const { xg = t.g(); }
 	__device__ __forceinline__ const char *row(int g, int r) const {
 		return W + (size_t)(g * R + r) * n * WT::BYTES;
 	}
@@ -132,26 +132,18 @@ struct PPush {
 	__device__ __forceinline__ void finish_pre(int g, const float *acc, const float *xr) const {
 #pragma unroll
 		for (int r = 0; r < R; ++r)
-			tpx_put(t, par, offset + g * R + r, xr[r] + acc[r]);
+			tpx_put(t, xg, offset + g * R + r, xr[r] + acc[r]);
 	}
 	__device__ __forceinline__ void finish_all(int g, const float *acc) const {
 #pragma unroll
 		for (int r = 0; r < R; ++r)
-			tpx_put(t, par, offset + g * R + r, (base ? base[g * R + r] : 0.0f) + acc[r]);
+			tpx_put(t, xg, offset + g * R + r, (base ? base[g * R + r] : 0.0f) + acc[r]);
 	}
 	__device__ __forceinline__ void finish(int g, const float *acc, int lane) const { // gemv_kernel
 		if (lane < R)
-			tpx_put(t, par, offset + g * R + lane, (base ? base[g * R + lane] : 0.0f) + acc[lane]);
+			tpx_put(t, xg, offset + g * R + lane, (base ? base[g * R + lane] : 0.0f) + acc[lane]);
 	}
-	static constexpr bool TAIL = true;
-	__device__ __forceinline__ void tail() const { tpx_arrive(t, gridDim.x); }
 };
-
-// policies with a tail() every thread runs after the epilogues (TAIL = true)
-template <class P, class = void>
-struct gemv_tail : std::false_type {};
-template <class P>
-struct gemv_tail<P, std::void_t<decltype(P::TAIL)>> : std::bool_constant<P::TAIL> {};
 
 // Virtual row space [wq | wk | wv]; a wave owns the RoPE pair (2g, 2g+1).
 template <class WT>
@@ -450,8 +442,6 @@ __global__ __launch_bounds__(GEMV_THREADS) void gemv_kernel(P p, const float *__
 			acc[r] = wave_sum(acc[r]);
 		p.finish(g, acc, lane);
 	}
-	if constexpr (gemv_tail<P>::value)
-		p.tail();
 }
 
 // Row-block GEMV — the production path (n % (64 * EPL) == 0).
@@ -551,7 +541,7 @@ __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__re
 	for (int i = threadIdx.x; i < ngl * R * W; i += THREADS)
 		part[i] = 0.0f;
 	if (tpx)
-		tpx_stage_x<NORM>(xs, tin, tpx_wait(tin), normw, n, eps);
+		tpx_stage_x<NORM>(xs, tin, tin.g(), normw, n, eps);
 	else if (xregs)
 		stage_x_regs<NORM, THREADS>(xs, xp, n, eps);
 	else
@@ -604,8 +594,6 @@ __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__re
 			p.finish_all(b + gl * NB, a);
 		}
 	}
-	if constexpr (gemv_tail<P>::value)
-		p.tail();
 #ifdef YALM_WG_TRACE // tools/wg_timeline.hip: per-workgroup start/end (s_memrealtime, 100 MHz)
 	if (threadIdx.x == 0) {
 		yalm_wg_trace[2 * b] = t_start;

@@ -16,26 +16,32 @@ __global__ void set_step_kernel(StepState *st, int token, int pos, int reset_gen
 		st->n_gen = 0;
 }
 
-// Explicit indices for the per-block test hook (Block::block signature).
-__global__ void set_step_full_kernel(StepState *st, int pos, int kv_sink, int kv_pos, int kv_len) {
+// Explicit indices for the per-block test hook (Block::block signature); n_ex: the IPC
+// tensor-parallel exchanges the block uses (tp_exchange.h).
+__global__ void set_step_full_kernel(StepState *st, int pos, int kv_sink, int kv_pos, int kv_len, int n_ex = 0) {
 	st->pos = pos;
 	st->kv_sink = kv_sink;
 	st->kv_pos = kv_pos;
 	st->kv_len = kv_len;
 	st->epoch = st->epoch + 1u;
+	st->xbase = st->xnext;
+	st->xnext = st->xnext + (unsigned)n_ex;
 }
 
 // Timing hook (yalm_time_kernel): a new launch generation, as step_begin_kernel
 // starts one, so an in-launch hand-off never sees the previous launch's tags.
-__global__ void epoch_bump_kernel(StepState *st) {
+__global__ void epoch_bump_kernel(StepState *st, int n_ex) {
 	st->epoch = st->epoch + 1u;
+	st->xbase = st->xnext;
+	st->xnext = st->xnext + (unsigned)n_ex;
 }
 
 // First node of every forward graph: sliding-window indices (infer.cu:1081-
-// 1083; KV_SINKS = 2, model.h:12) and x = embedding[token] (infer.cu:622-640).
+// 1083; KV_SINKS = 2, model.h:12) and x = embedding[token] (infer.cu:622-640);
+// n_ex: the IPC tensor-parallel exchanges this forward uses (tp_exchange.h).
 template <class WT>
 __global__ __launch_bounds__(256) void step_begin_kernel(StepState *st, const void *__restrict__ emb, int dim,
-                                                         float *__restrict__ x, int max_seq_len) {
+                                                         float *__restrict__ x, int max_seq_len, int n_ex) {
 	const int token = st->token;
 	const int pos = st->pos;
 	const char *row = (const char *)emb + (size_t)token * dim * WT::BYTES;
@@ -52,6 +58,8 @@ __global__ __launch_bounds__(256) void step_begin_kernel(StepState *st, const vo
 		st->kv_pos = kv_sink + (pos - kv_sink) % (max_seq_len - kv_sink);
 		st->kv_len = pos >= max_seq_len ? max_seq_len : pos + 1;
 		st->epoch = st->epoch + 1u;
+		st->xbase = st->xnext;
+		st->xnext = st->xnext + (unsigned)n_ex;
 	}
 }
 
@@ -159,57 +167,68 @@ __global__ __launch_bounds__(1024) void argmax_kernel(const float *__restrict__ 
 // the exchange and the pick inside the argmax launch, identical on every rank.
 __global__ __launch_bounds__(1024) void argmax_tp_kernel(const float *__restrict__ logits, int n, StepState *st,
                                                          int *__restrict__ tokens_out, int cap, TpX t) {
+	const unsigned g = t.g();
 	float b = 0.0f;
 	int idx = 0;
 	argmax_block(logits, n, b, idx);
 	if (threadIdx.x == 0) {
-		const unsigned par = tpx_seq(t) & 1u;
-		tpx_put(t, par, 0, b);
-		tpx_put(t, par, 1, __int_as_float(idx + t.rank * n));
-	}
-	tpx_arrive(t, 1);
-	if (threadIdx.x < 64) {
-		const unsigned par = tpx_wait(t);
-		if (threadIdx.x == 0) {
-			float bb = 0.0f;
-			int bi = 0;
-			for (int p = 0; p < t.n; ++p) {
-				const float *pr = t.slot(t.rank, par, p);
-				const float v = tpx_ldf(pr);
-				const int j = __float_as_int(tpx_ldf(pr + 1));
-				if (p == 0 || v > bb || (v == bb && j < bi)) {
-					bb = v;
-					bi = j;
-				}
+		tpx_put(t, g, 0, b);
+		tpx_put(t, g, 1, __int_as_float(idx + t.rank * n));
+		const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + TPX_TIMEOUT;
+		float bb = 0.0f;
+		int bi = 0;
+		for (int p = 0; p < t.n; ++p) {
+			const float v = tpx_get1(t, g, p, 0, deadline);
+			const int j = __float_as_int(tpx_get1(t, g, p, 1, deadline));
+			if (p == 0 || v > bb || (v == bb && j < bi)) {
+				bb = v;
+				bi = j;
 			}
-			argmax_commit(st, bi, tokens_out, cap);
 		}
+		argmax_commit(st, bi, tokens_out, cap);
 	}
+}
+
+// Every granule of exchange g (n per rank) has arrived, checked by one wave (bounded).
+__device__ __forceinline__ void tpx_wait_all(const TpX &t, unsigned g, int n) {
+	const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + TPX_TIMEOUT;
+	for (int p = 0; p < t.n; ++p)
+		for (int i = threadIdx.x; i < n; i += blockDim.x)
+			(void)tpx_get1(t, g, p, i, deadline);
 }
 
 // Tensor parallelism over IPC, ranks sharing one GPU: wait for the exchange in one wave
 // before the consumer launch (yalm_hip.hip tpx_consume).
-__global__ __launch_bounds__(64) void tpx_gate_kernel(TpX t) {
-	(void)tpx_wait(t);
+__global__ __launch_bounds__(64) void tpx_gate_kernel(TpX t, int n) {
+	tpx_wait_all(t, t.g(), n);
 }
 
 // Tensor parallelism over IPC: the consumer side of one exchange as a launch of its own --
 // the summed x into `out` (yalm_block's result; the timing hook of the exchange), or, with
 // gather, the n floats of every rank's slot side by side (the sharded logits).
 __global__ __launch_bounds__(1024) void tpx_collect_kernel(TpX t, int n, int gather, float *__restrict__ out) {
-	const unsigned par = tpx_wait(t);
+	const unsigned g = t.g();
+	const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + TPX_TIMEOUT;
 	if (gather) {
 		for (int p = 0; p < t.n; ++p)
 			for (int i = threadIdx.x; i < n; i += blockDim.x)
-				out[(size_t)p * n + i] = tpx_ldf(t.slot(t.rank, par, p) + i);
+				out[(size_t)p * n + i] = tpx_get1(t, g, p, i, deadline);
 		return;
 	}
 	for (int i = threadIdx.x; i < n; i += blockDim.x) {
-		float s = tpx_ldf(t.slot(t.rank, par, 0) + i);
+		float s = tpx_get1(t, g, 0, i, deadline);
 		for (int p = 1; p < t.n; ++p)
-			s += tpx_ldf(t.slot(t.rank, par, p) + i);
+			s += tpx_get1(t, g, p, i, deadline);
 		out[i] = s;
 	}
+}
+
+// Timing hook (yalm_time_kernel id 6 under IPC): a producer of exchange g alone -- this
+// rank's x pushed to every rank's slot -- for the collect launch that follows.
+__global__ __launch_bounds__(1024) void tpx_push_kernel(TpX t, int n, const float *__restrict__ x) {
+	const unsigned g = t.g();
+	for (int i = threadIdx.x; i < n; i += blockDim.x)
+		tpx_put(t, g, i, x[i]);
 }
 
 // Tensor parallelism: pick the global first maximum from the tp_size gathered

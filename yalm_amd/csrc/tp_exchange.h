@@ -8,139 +8,134 @@
 // and summed every rank's partial: 2 exchanges x (launch + round trips) per layer, 7
 // launches per layer against 4 on one GPU. Here there is no exchange kernel:
 //   * PRODUCER (the Wo workgroups of the fused attention + Wo launch, the W2 GEMV, the
-//     argmax): each workgroup PUSHES its rows to slot [parity][this rank] of EVERY
-//     rank's buffer (system-scope stores: the bytes leave the writer at once), waits for
-//     them (vmcnt(0)), and takes a ticket; the last workgroup of the launch bumps
-//     xdone[this rank] in every rank's control words.
+//     argmax, the logits GEMV of an OUTPUT forward): each row value is PUSHED to slot
+//     [parity][this rank] of EVERY rank's buffer as an 8-byte {value, tag} granule, ONE
+//     system-scope store each: the data is its own ready flag (the granule hand-off of
+//     attn_wo.h, across processes) -- no drain, no counter, no last-arriver.
 //   * CONSUMER (the next GEMV's x staging: GLU after Wo, next layer's QKV / the logits
-//     after W2): waits until xdone[p] >= xdone[own] for every rank p (this rank's own
-//     count is final: its producer finished before the consumer launched), then sums
-//     the N slots in rank order -- bit-identical x on every rank -- while its weight
-//     stream is already in flight, and writes x back for the next residual.
-// Strict alternation of the two parities holds by construction: exchange k uses parity
-// k & 1 where k = this rank's produced-exchange count, and a peer's producer k + 2 (same
-// parity) can only start after its consumer k + 1, which needs this rank's producer k + 1,
-// which runs after this rank's consumer k. Every rank runs the same exchange sequence
-// (the API's lockstep rule), whatever the graph (HYDRATE / LOGITS / GREEDY, yalm_block):
-// no sequence number is derived from the forward's structure.
+//     after W2): loads the N slots' granules of its x, re-reading until every tag is this
+//     exchange's, sums them in rank order -- bit-identical x on every rank -- while its
+//     weight stream is already in flight, and (workgroup 0) writes x back for the next
+//     residual.
+// The exchange index g = StepState.xbase + ex: step_begin_kernel (and yalm_block's
+// set_step_full_kernel, the timing hooks' bump) reserves this forward's exchanges
+// [xbase, xbase + n_ex) and every launch knows its own ex statically (Wo of layer l:
+// 2 l, W2: 2 l + 1, the logits / argmax: 2 L). Exchange g uses parity g & 1 and tag g + 1
+// (zeroed memory never matches). Consecutive exchanges alternate parity, and a peer's
+// producer g + 2 (the same parity) runs only after its consumer g + 1, which needs this
+// rank's producer g + 1, which runs after this rank's consumer g: a slot is never
+// rewritten while it is read. Every rank runs the same exchange sequence (the API's
+// lockstep rule).
+//
+// Round 5 first cut (measured, TP1 on one MI355X, rocprofv3): per-rank exchange counters
+// bumped by the producer launch's last workgroup (drain, ticket, fence, remote atomics)
+// and a counter poll before the consumer's loads cost +4.2 us per W2, +5.2 per attention
+// + Wo, +1.8 / +2.2 per GLU / QKV launch over one GPU -- three serialised round trips at
+// every producer's tail. Granules leave one.
 //
 // Buffer per rank (yalm_tp_ipc_alloc, hipDeviceMallocUncached: never cached in a
-// reader's L2, so a pushed value cannot be shadowed by a stale line), mapped on every
-// rank: [2 parities][n ranks][S floats] slots, then control words: xdone[64] (exchanges
-// produced by each source rank, toward this rank), ticket, error.
+// reader's L2, so a pushed granule cannot be shadowed by a stale line), mapped on every
+// rank: [2 parities][n ranks][S granules], then control words (error).
 #pragma once
 
 #include "device_common.h"
 
 #define TPX_TIMEOUT 200000000ull // 2 s of s_memrealtime (100 MHz)
-#define TPX_CTRL_WORDS 128       // xdone[64], ticket, error, padding
+#define TPX_CTRL_WORDS 64        // error word + padding (in floats)
 
 struct TpX {
-	float *const *bufs; // [n] this rank's buffer and the peers' (IPC-mapped), device array
-	int rank, n, S;     // this rank, ranks, floats per (parity, source) slot
-	float *xw;          // consumer: where the summed x is written back (the decoder's x)
-	__device__ __forceinline__ unsigned *ctrl(int p) const {
-		return (unsigned *)(bufs[p] + 2 * (size_t)n * S);
+	float *const *bufs;     // [n] this rank's buffer and the peers' (IPC-mapped), device array
+	int rank, n, S;         // this rank, ranks, granules per (parity, source) slot
+	float *xw;              // consumer: where the summed x is written back (the decoder's x)
+	const StepState *step;  // xbase: this forward's first exchange index
+	int ex;                 // this launch's exchange within the forward
+	__device__ __forceinline__ unsigned long long *slot(int p, unsigned par, int src) const {
+		return (unsigned long long *)bufs[p] + ((size_t)(par & 1u) * n + src) * S;
 	}
-	__device__ __forceinline__ float *slot(int p, unsigned par, int src) const {
-		return bufs[p] + ((size_t)(par & 1u) * n + src) * S;
+	__device__ __forceinline__ unsigned *err() const {
+		return (unsigned *)((unsigned long long *)bufs[rank] + 2 * (size_t)n * S);
 	}
+	// this launch's exchange index (one load of the step state, a kernel-start read)
+	__device__ __forceinline__ unsigned g() const { return step->xbase + (unsigned)ex; }
 };
 
-__device__ __forceinline__ unsigned tpx_ld(const unsigned *p) {
-	return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ void tpx_st(float *p, float v) {
-	__hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ float tpx_ldf(const float *p) {
-	return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// Exchanges this rank has produced so far; a producer pushes into parity tpx_seq & 1.
-__device__ __forceinline__ unsigned tpx_seq(const TpX &t) {
-	return tpx_ld(t.ctrl(t.rank) + t.rank);
-}
-
-// Producer: element i of this rank's slot, on every rank (own first).
-__device__ __forceinline__ void tpx_put(const TpX &t, unsigned par, int i, float v) {
+// Producer: element i of this rank's slot of exchange g, on every rank (own first).
+__device__ __forceinline__ void tpx_put(const TpX &t, unsigned g, int i, float v) {
+	const unsigned long long gr = (unsigned long long)__float_as_uint(v) | ((unsigned long long)(g + 1u) << 32);
 	for (int k = 0; k < t.n; ++k) {
 		const int p = t.rank + k < t.n ? t.rank + k : t.rank + k - t.n;
-		tpx_st(t.slot(p, par, t.rank) + i, v);
+		__hip_atomic_store(t.slot(p, g, t.rank) + i, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 	}
 }
 
-// Producer tail, called by every thread of each of the launch's `nprod` producer
-// workgroups after its pushes: the stores are drained (their writes acknowledged), the
-// workgroup takes a ticket; the last one resets the ticket and bumps xdone[rank] on
-// every rank.
-__device__ __forceinline__ void tpx_arrive(const TpX &t, int nprod) {
-	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-	__syncthreads();
-	if (threadIdx.x == 0) {
-		unsigned *tk = t.ctrl(t.rank) + 64;
-		const unsigned v = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
-		if (v == (unsigned)nprod - 1u) {
-			__hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-			__builtin_amdgcn_fence(__ATOMIC_RELEASE, ""); // every workgroup's pushes before the counts
-			for (int k = 0; k < t.n; ++k) {
-				const int p = t.rank + k < t.n ? t.rank + k : t.rank + k - t.n;
-				__hip_atomic_fetch_add(t.ctrl(p) + t.rank, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-			}
-		}
-	}
-}
-
-// Consumer: every wave waits (lane p polls rank p's count) until each rank has produced
-// as many exchanges as this rank; returns the parity to read. A wait past TPX_TIMEOUT
-// gives up (results wrong) and sets the error word, reported by the next sync call.
-__device__ __forceinline__ unsigned tpx_wait(const TpX &t) {
-	const unsigned *c = t.ctrl(t.rank);
-	const unsigned want = tpx_ld(c + t.rank);
-	const int lane = threadIdx.x & 63;
-	const unsigned *mine = c + (lane < t.n ? lane : t.rank);
-	const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + TPX_TIMEOUT;
+// Consumer: one granule of source rank src (element i) of exchange g, waited for (bounded;
+// a wait that gives up sets the error word, reported by the next sync call).
+__device__ __forceinline__ float tpx_get1(const TpX &t, unsigned g, int src, int i, unsigned long long deadline) {
+	const unsigned long long *s = t.slot(t.rank, g, src) + i;
 	for (;;) {
-		if (__all((int)(tpx_ld(mine) - want) >= 0))
-			break;
-		__builtin_amdgcn_s_sleep(1);
+		const unsigned long long v = __hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+		if ((unsigned)(v >> 32) == g + 1u)
+			return __uint_as_float((unsigned)v);
 		if (__builtin_amdgcn_s_memrealtime() > deadline) {
-			if (lane == 0)
-				__hip_atomic_store((unsigned *)c + 65, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-			break;
+			__hip_atomic_store(t.err(), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+			return __uint_as_float((unsigned)v);
 		}
+		__builtin_amdgcn_s_sleep(1);
 	}
-	return (want - 1u) & 1u;
 }
 
-// Consumer: the summed x (rank order) of parity par into LDS xs[0, n), optionally
+// Consumer: the summed x (rank order) of exchange g into LDS xs[0, n), optionally
 // rmsnorm'ed (infer.cpp:134-144, the statement order of stage_x), and workgroup 0 writes
-// the raw sum back to t.xw. Four floats per thread per pass; every rank's loads issued
-// before the adds.
+// the raw sum back to t.xw. Per pass a thread loads 4 elements of every rank (2 x 16-byte
+// sc0 sc1 loads of 2 granules each, through a buffer resource so the compiler tracks
+// them), all issued before any check; a pass re-reads until every tag in the wave is g + 1.
 template <bool NORM, int NMAX = 8>
-__device__ __forceinline__ void tpx_stage_x(float *xs, const TpX &t, unsigned par, const float *__restrict__ normw,
+__device__ __forceinline__ void tpx_stage_x(float *xs, const TpX &t, unsigned g, const float *__restrict__ normw,
                                             int n, float eps) {
 	const int tid = threadIdx.x, nthreads = blockDim.x;
-	// the own buffer through a buffer resource: 16-byte sc0 sc1 (system-scope) loads the
-	// compiler tracks (cachepolicy 0x11), instead of four 4-byte atomic loads each
 	const uint64_t ba = (uint64_t)t.bufs[t.rank];
 	const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)ba), hi = __builtin_amdgcn_readfirstlane((uint32_t)(ba >> 32));
 	const __amdgpu_buffer_rsrc_t own = __builtin_amdgcn_make_buffer_rsrc(
-	    (void *)(((uint64_t)hi << 32) | lo), (short)0, (int)(2u * (uint32_t)t.n * (uint32_t)t.S * 4u), 0x00020000);
-	const uint32_t base = ((par & 1u) * (uint32_t)t.n) * (uint32_t)t.S * 4u, rstride = (uint32_t)t.S * 4u;
+	    (void *)(((uint64_t)hi << 32) | lo), (short)0, (int)(2u * (uint32_t)t.n * (uint32_t)t.S * 8u), 0x00020000);
+	const uint32_t base = ((g & 1u) * (uint32_t)t.n) * (uint32_t)t.S * 8u, rstride = (uint32_t)t.S * 8u;
+	const unsigned tag = g + 1u;
+	const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + TPX_TIMEOUT;
 	float ss = 0.0f;
 	for (int i = tid * 4; i < n; i += nthreads * 4) {
-		float4_t v[NMAX];
+		u32x4_t v[NMAX][2];
+		for (;;) {
 #pragma unroll
-		for (int r = 0; r < NMAX; ++r)
-			if (r < t.n)
-				v[r] = __builtin_bit_cast(float4_t, __builtin_amdgcn_raw_buffer_load_b128(
-				                                        own, base + (uint32_t)r * rstride + (uint32_t)i * 4u, 0, 0x11));
-		float4_t a = v[0];
+			for (int r = 0; r < NMAX; ++r)
+				if (r < t.n) {
+					const uint32_t o = base + (uint32_t)r * rstride + (uint32_t)i * 8u;
+					v[r][0] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(own, o, 0, 0x11));
+					v[r][1] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(own, o + 16u, 0, 0x11));
+				}
+			bool ok = true;
+#pragma unroll
+			for (int r = 0; r < NMAX; ++r)
+				if (r < t.n)
+					ok = ok && v[r][0][1] == tag && v[r][0][3] == tag && v[r][1][1] == tag && v[r][1][3] == tag;
+			if (__all(ok))
+				break;
+			if (__builtin_amdgcn_s_memrealtime() > deadline) {
+				if ((tid & 63) == 0)
+					__hip_atomic_store(t.err(), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+				break;
+			}
+			__builtin_amdgcn_s_sleep(1);
+		}
+		float4_t a;
+		{
+			const uint32_t e0 = v[0][0][0], e1 = v[0][0][2], e2 = v[0][1][0], e3 = v[0][1][2];
+			a = float4_t{__uint_as_float(e0), __uint_as_float(e1), __uint_as_float(e2), __uint_as_float(e3)};
+		}
 #pragma unroll
 		for (int r = 1; r < NMAX; ++r)
-			if (r < t.n)
-				a += v[r];
+			if (r < t.n) {
+				const uint32_t e0 = v[r][0][0], e1 = v[r][0][2], e2 = v[r][1][0], e3 = v[r][1][2];
+				a += float4_t{__uint_as_float(e0), __uint_as_float(e1), __uint_as_float(e2), __uint_as_float(e3)};
+			}
 		*(float4_t *)(xs + i) = a;
 		if (blockIdx.x == 0)
 			*(float4_t *)(t.xw + i) = a;

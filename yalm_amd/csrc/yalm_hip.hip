@@ -472,7 +472,7 @@ int awo_check(yalm_decoder_s *d) {
 		}
 	}
 	if (d->ipc) { // tp_exchange.h: a consumer's bounded wait for a peer's exchange gave up
-		unsigned *flag = (unsigned *)(d->ipc_own + 2 * (size_t)d->tp_size * d->ipc_S) + 65;
+		unsigned *flag = (unsigned *)((unsigned long long *)d->ipc_own + 2 * (size_t)d->tp_size * d->ipc_S); // TpX::err
 		unsigned e = 0;
 		HIPCHK(hipMemcpy(&e, flag, sizeof(e), hipMemcpyDeviceToHost));
 		if (e) {
@@ -482,6 +482,14 @@ int awo_check(yalm_decoder_s *d) {
 		}
 	}
 	return YALM_OK;
+}
+
+// The exchange descriptor of a launch taking part in exchange `ex` of the current launch
+// sequence (tp_exchange.h: g = StepState.xbase + ex).
+static TpX tpx_ex(const yalm_decoder_s *d, int ex) {
+	TpX t = d->tpx;
+	t.ex = ex;
+	return t;
 }
 
 template <class WT, int GT, int KB>
@@ -501,9 +509,9 @@ static void launch_attn_wo_g(yalm_decoder_s *d, const yalm_block_weights &w, con
 }
 // The fused attention + Wo launch of one layer. One GPU: x += Wo attn(q). Tensor parallel:
 // the rank's partial (+ x on rank 0) -- into xs, then the RCCL all-reduce into x; or pushed
-// to the IPC exchange (consumed by the GLU GEMV's x staging, tp_exchange.h).
+// to the IPC exchange `ex` (consumed by the GLU GEMV's x staging, tp_exchange.h).
 template <class WT>
-static int launch_attn_wo(yalm_decoder_s *d, const yalm_block_weights &w, int layer) {
+static int launch_attn_wo(yalm_decoder_s *d, const yalm_block_weights &w, int layer, int ex) {
 	const yalm_config &c = d->c;
 	AttnWoArgs p;
 	p.n_heads = c.n_heads;
@@ -522,7 +530,7 @@ static int launch_attn_wo(yalm_decoder_s *d, const yalm_block_weights &w, int la
 	p.x = d->x;
 	p.out = d->comm ? d->xs : d->x;
 	p.add_base = d->tp_rank == 0;
-	p.push = d->ipc ? d->tpx : TpX{};
+	p.push = d->ipc ? tpx_ex(d, ex) : TpX{};
 	p.err = d->awo_err;
 	p.trace = d->awo_trace;
 	p.delay = d->awo_delay;
@@ -550,12 +558,14 @@ static int launch_attn_wo(yalm_decoder_s *d, const yalm_block_weights &w, int la
 	return YALM_OK;
 }
 
-// One tensor-parallel exchange of x alone, as a launch of its own: timing hook for the
-// communication cost (yalm_time_kernel id 6). RCCL: one all-reduce. IPC: the consumer side
-// (wait for every rank + sum into x) -- in the forward it runs inside the next GEMV.
+// One tensor-parallel exchange of x alone, as launches of their own: timing hook for the
+// communication cost (yalm_time_kernel id 6). RCCL: one all-reduce. IPC: x pushed to every
+// rank, then the consumer side (wait for every rank + sum) -- in the forward the push is the
+// producer GEMV's epilogue and the sum runs inside the next GEMV's x staging.
 static int enqueue_exchange(yalm_decoder_s *d) {
 	if (d->ipc) {
-		tpx_collect_kernel<<<1, 1024, 0, d->stream>>>(d->tpx, d->c.dim, 0, d->x);
+		tpx_push_kernel<<<1, 1024, 0, d->stream>>>(tpx_ex(d, 0), d->c.dim, d->x);
+		tpx_collect_kernel<<<1, 1024, 0, d->stream>>>(tpx_ex(d, 0), d->c.dim, 0, d->xs);
 		HIPCHK(hipGetLastError());
 		return YALM_OK;
 	}
@@ -574,22 +584,24 @@ static int enqueue_exchange(yalm_decoder_s *d) {
 // rank's input columns: rank 0's partial carries x. RCCL: rank 0 writes xs = x + W v, the
 // others xs = W v, and one all-reduce (sum, captured in the graph) lands the sum in x on
 // every rank (identical bits). IPC: the partial is pushed to every rank's exchange slot
-// (PPush, tp_exchange.h); the next GEMV sums the slots while its weights stream in.
+// (PPush, exchange `ex`, tp_exchange.h); the next GEMV sums the slots while its weights
+// stream in. ex < 0 under IPC: a result nothing reads (the last W2 of a hydration forward)
+// stays local -- an exchange nobody consumes would break the slot-reuse order.
 template <class WT>
-static int enqueue_residual_gemv(yalm_decoder_s *d, const void *W, int n, const float *v, int kind) {
+static int enqueue_residual_gemv(yalm_decoder_s *d, const void *W, int n, const float *v, int kind, int ex) {
 	const yalm_config &c = d->c;
 	hipStream_t st = d->stream;
-	if (d->ipc) {
+	if (d->ipc && ex >= 0) {
 		PPush<WT, 1> p;
 		p.W = (const char *)W;
 		p.n = n;
 		p.base = d->tp_rank == 0 ? d->x : nullptr;
-		p.t = d->tpx;
+		p.t = tpx_ex(d, ex);
 		p.offset = 0;
 		p.n_groups = c.dim;
 		return launch_gemv<WT, PPush<WT, 1>, false>(p, v, nullptr, 0.f, kind, d->gemv[kind], st);
 	}
-	if (!d->comm) {
+	if (!d->comm) { // one GPU (or the unread IPC case above)
 		PResidual<WT, 1> p;
 		p.W = (const char *)W;
 		p.n = n;
@@ -625,17 +637,18 @@ static int enqueue_residual_gemv(yalm_decoder_s *d, const void *W, int n, const 
 // first: a consumer whose 256 workgroups spin in tpx_wait could otherwise hold every CU a
 // peer's producer needs (a deadlock the bounded wait only reports). One GPU per rank (the
 // real configuration) needs no gate: the consumer waits inside its own launch.
-static TpX tpx_consume(yalm_decoder_s *d) {
+static TpX tpx_consume(yalm_decoder_s *d, int ex, int n) {
 	if (d->tpx_gate)
-		tpx_gate_kernel<<<1, 64, 0, d->stream>>>(d->tpx);
-	return d->tpx;
+		tpx_gate_kernel<<<1, 64, 0, d->stream>>>(tpx_ex(d, ex), n);
+	return tpx_ex(d, ex);
 }
 
-// One layer. x_exchanged: the layer's input x is the previous layer's W2 exchange (IPC
-// tensor parallelism: the QKV GEMV consumes it), not a local x (the embedding of layer 0,
-// or the x yalm_block / yalm_set_x left).
+// One layer. IPC tensor parallelism (tp_exchange.h): the Wo partial is exchange ex0 (the GLU
+// consumes it), the W2 partial exchange ex0 + 1 (push_w2; the next QKV or the logits GEMV
+// consumes it); x_exchanged: the layer's input x is exchange ex0 - 1 (the QKV GEMV consumes
+// it), not a local x (the embedding of layer 0, or the x yalm_block / yalm_set_x left).
 template <class WT>
-static int enqueue_layer_t(yalm_decoder_s *d, int l, bool x_exchanged) {
+static int enqueue_layer_t(yalm_decoder_s *d, int l, int ex0, bool x_exchanged, bool push_w2) {
 	const yalm_config &c = d->c;
 	const yalm_block_weights &w = d->b[l];
 	hipStream_t st = d->stream;
@@ -658,14 +671,14 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l, bool x_exchanged) {
 		p.kcache = w.key_cache;
 		p.vcache = w.value_cache;
 		TRY((launch_gemv_d<WT, PQKV<WT>, true>(d, p, d->x, w.rms_att, c.norm_eps, GK_QKV,
-		                                         d->ipc && x_exchanged ? tpx_consume(d) : none)));
+		                                         d->ipc && x_exchanged ? tpx_consume(d, ex0 - 1, c.dim) : none)));
 	}
 	if (d->attn_wo && WT::BYTES <= 2) {
-		TRY(launch_attn_wo<WT>(d, w, l));
+		TRY(launch_attn_wo<WT>(d, w, l, ex0));
 	} else {
 		TRY(launch_attn(c.head_dim, c.n_heads, c.n_kv_heads, d->q, w.key_cache, w.value_cache, d->step, c.max_seq_len,
 		                d->part, l, c.n_layers, d->awo_err, nullptr, d->xb2, st));
-		TRY(enqueue_residual_gemv<WT>(d, w.wo, q_dim, d->xb2, GK_WO));
+		TRY(enqueue_residual_gemv<WT>(d, w.wo, q_dim, d->xb2, GK_WO, ex0));
 	}
 	// the GLU consumes the Wo exchange under IPC tensor parallelism
 	if (c.act == YALM_SILU) {
@@ -675,7 +688,7 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l, bool x_exchanged) {
 		p.n = c.dim;
 		p.out = d->hb;
 		p.n_groups = c.hidden_dim;
-		TRY((launch_gemv_d<WT, PGlu<WT, 1>, true>(d, p, d->x, w.rms_ffn, c.norm_eps, GK_GLU, d->ipc ? tpx_consume(d) : none)));
+		TRY((launch_gemv_d<WT, PGlu<WT, 1>, true>(d, p, d->x, w.rms_ffn, c.norm_eps, GK_GLU, d->ipc ? tpx_consume(d, ex0, c.dim) : none)));
 	} else {
 		PGlu<WT, 0> p;
 		p.w1 = (const char *)w.w1;
@@ -683,24 +696,24 @@ static int enqueue_layer_t(yalm_decoder_s *d, int l, bool x_exchanged) {
 		p.n = c.dim;
 		p.out = d->hb;
 		p.n_groups = c.hidden_dim;
-		TRY((launch_gemv_d<WT, PGlu<WT, 0>, true>(d, p, d->x, w.rms_ffn, c.norm_eps, GK_GLU, d->ipc ? tpx_consume(d) : none)));
+		TRY((launch_gemv_d<WT, PGlu<WT, 0>, true>(d, p, d->x, w.rms_ffn, c.norm_eps, GK_GLU, d->ipc ? tpx_consume(d, ex0, c.dim) : none)));
 	}
-	return enqueue_residual_gemv<WT>(d, w.w2, c.hidden_dim, d->hb, GK_W2);
+	return enqueue_residual_gemv<WT>(d, w.w2, c.hidden_dim, d->hb, GK_W2, push_w2 ? ex0 + 1 : -1);
 }
 
-// Final norm + classifier rows of this rank. IPC tensor parallelism: consume = the GEMV
-// consumes the last layer's W2 exchange; push (OUTPUT_LOGITS) = it also produces the logits
-// gather, this rank's vocabulary rows pushed to every rank's slot.
+// Final norm + classifier rows of this rank. IPC tensor parallelism: consume_ex >= 0 = the
+// GEMV consumes that exchange (the last layer's W2); push_ex >= 0 (OUTPUT_LOGITS) = it also
+// produces that exchange, the logits gather: this rank's vocabulary rows pushed to every rank.
 template <class WT>
-static int enqueue_logits_t(yalm_decoder_s *d, bool consume, bool push) {
+static int enqueue_logits_t(yalm_decoder_s *d, int consume_ex, int push_ex) {
 	const yalm_config &c = d->c;
-	const TpX tin = consume ? tpx_consume(d) : TpX{};
-	if (push) {
+	const TpX tin = consume_ex >= 0 ? tpx_consume(d, consume_ex, c.dim) : TpX{};
+	if (push_ex >= 0) {
 		PPush<WT, 1> p;
 		p.W = (const char *)d->wcls;
 		p.n = c.dim;
 		p.base = nullptr;
-		p.t = d->tpx;
+		p.t = tpx_ex(d, push_ex);
 		p.offset = 0;
 		p.n_groups = c.vocab_size;
 		return launch_gemv<WT, PPush<WT, 1>, true>(p, d->x, d->rms_final, c.norm_eps, GK_CLS, d->gemv[GK_CLS],
@@ -723,8 +736,8 @@ static int enqueue_logits_t(yalm_decoder_s *d, bool consume, bool push) {
 }
 
 template <class WT>
-static int enqueue_begin_t(yalm_decoder_s *d) {
-	step_begin_kernel<WT><<<1, 256, 0, d->stream>>>(d->step, d->emb, d->c.dim, d->x, d->c.max_seq_len);
+static int enqueue_begin_t(yalm_decoder_s *d, int n_ex) {
+	step_begin_kernel<WT><<<1, 256, 0, d->stream>>>(d->step, d->emb, d->c.dim, d->x, d->c.max_seq_len, n_ex);
 	HIPCHK(hipGetLastError());
 	return YALM_OK;
 }
@@ -734,22 +747,29 @@ static int enqueue_begin_t(yalm_decoder_s *d) {
 	 : (dtype) == YALM_F16 ? FN<WF16>(__VA_ARGS__)                                                                     \
 	                       : FN<WF8>(__VA_ARGS__))
 
+// IPC tensor parallelism (tp_exchange.h): layer l's Wo and W2 partials are exchanges 2 l and
+// 2 l + 1, the logits gather / argmax pairs exchange 2 L. Every exchange of the sequence is
+// consumed (the slot-reuse order relies on it), so a hydration forward keeps its last W2
+// local: 2 L - 1 exchanges, 2 L + 1 with an output.
 static int enqueue_forward(yalm_decoder_s *d, int which) {
-	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_begin_t, d));
-	for (int l = 0; l < d->c.n_layers; ++l)
-		TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_layer_t, d, l, l > 0));
-	if (which == GRAPH_HYDRATE)
+	const int L = d->c.n_layers;
+	const bool hyd = which == GRAPH_HYDRATE;
+	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_begin_t, d, d->ipc ? (hyd ? 2 * L - 1 : 2 * L + 1) : 0));
+	for (int l = 0; l < L; ++l)
+		TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_layer_t, d, l, 2 * l, l > 0, !(hyd && l == L - 1)));
+	if (hyd)
 		return YALM_OK;
-	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_logits_t, d, d->ipc, d->ipc && which == GRAPH_LOGITS));
+	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_logits_t, d, d->ipc ? 2 * L - 1 : -1,
+	                d->ipc && which == GRAPH_LOGITS ? 2 * L : -1));
 	if (d->ipc) { // tp_exchange.h: no exchange launches
 		if (which == GRAPH_LOGITS) { // every rank's vocabulary slice, side by side
-			tpx_collect_kernel<<<1, 1024, 0, d->stream>>>(d->tpx, d->c.vocab_size, 1, d->logits);
+			tpx_collect_kernel<<<1, 1024, 0, d->stream>>>(tpx_ex(d, 2 * L), d->c.vocab_size, 1, d->logits);
 			HIPCHK(hipGetLastError());
 			HIPCHK(hipMemcpyAsync(d->logits_pinned, d->logits, sizeof(float) * d->vocab_full, hipMemcpyDeviceToHost,
 			                      d->stream));
 		} else { // local first max, pushed; every rank's pair gathered and picked in the same launch
 			argmax_tp_kernel<<<1, 1024, 0, d->stream>>>(d->logits_local, d->c.vocab_size, d->step, d->tokens,
-			                                            d->tokens_cap, d->tpx);
+			                                            d->tokens_cap, tpx_ex(d, 2 * L));
 			HIPCHK(hipGetLastError());
 		}
 		return YALM_OK;
@@ -976,13 +996,14 @@ static int tp_local_config(const yalm_config &f, int tp_size, yalm_config &lc) {
 	return YALM_OK;
 }
 
-// floats per (parity, source rank) slot of the IPC exchange: x, or a rank's vocabulary rows
+// {value, tag} granules per (parity, source rank) slot of the IPC exchange: x, or a rank's
+// vocabulary rows (tp_exchange.h)
 static int ipc_slot_floats(const yalm_config &f, int tp_size) {
 	const int need = std::max(f.dim, f.vocab_size / tp_size + 2);
 	return (need + 63) / 64 * 64;
 }
 static size_t ipc_buf_bytes(const yalm_config &f, int tp_size) {
-	return (2 * (size_t)tp_size * ipc_slot_floats(f, tp_size) + TPX_CTRL_WORDS) * sizeof(float);
+	return 2 * (size_t)tp_size * ipc_slot_floats(f, tp_size) * sizeof(unsigned long long) + TPX_CTRL_WORDS * sizeof(float);
 }
 
 extern "C" int yalm_tp_unique_id(void *id_out) {
@@ -1097,6 +1118,8 @@ extern "C" int yalm_decoder_create_tp_ipc(const yalm_config *config, const yalm_
 	d->tpx.n = tp_size;
 	d->tpx.S = d->ipc_S;
 	d->tpx.xw = d->x;
+	d->tpx.step = d->step;
+	d->tpx.ex = 0;
 	return YALM_OK;
 }
 
@@ -1200,11 +1223,11 @@ extern "C" int yalm_block(yalm_decoder d, int layer, int pos, int kv_sink, int k
 	ARGCHK(d && layer >= 0 && layer < d->c.n_layers, "bad layer");
 	ARGCHK(kv_len >= 1 && kv_len <= d->c.max_seq_len && kv_pos >= 0 && kv_pos < d->c.max_seq_len,
 	       "bad kv indices");
-	set_step_full_kernel<<<1, 1, 0, d->stream>>>(d->step, pos, kv_sink, kv_pos, kv_len);
+	set_step_full_kernel<<<1, 1, 0, d->stream>>>(d->step, pos, kv_sink, kv_pos, kv_len, d->ipc ? 2 : 0);
 	HIPCHK(hipGetLastError());
-	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_layer_t, d, layer, false));
+	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_layer_t, d, layer, 0, false, true));
 	if (d->ipc) { // the layer's W2 pushed its partial: collect the sum into x (a forward's next GEMV would)
-		tpx_collect_kernel<<<1, 1024, 0, d->stream>>>(d->tpx, d->c.dim, 0, d->x);
+		tpx_collect_kernel<<<1, 1024, 0, d->stream>>>(tpx_ex(d, 1), d->c.dim, 0, d->x);
 		HIPCHK(hipGetLastError());
 	}
 	HIPCHK(hipStreamSynchronize(d->stream));
@@ -1282,12 +1305,12 @@ static int enqueue_one_t(yalm_decoder_s *d, int kernel_id, int l) {
 		return launch_attn(c.head_dim, c.n_heads, c.n_kv_heads, d->q, w.key_cache, w.value_cache, d->step,
 		                   c.max_seq_len, d->part, l, c.n_layers, d->awo_err, nullptr, d->xb2, d->stream);
 	case 5: // (local x: the timing hooks never take part in an exchange, except kernels 6 and 8)
-		return enqueue_logits_t<WT>(d, false, false);
+		return enqueue_logits_t<WT>(d, -1, -1);
 	case 6:
 		return enqueue_exchange(d);
-	case 8: // fused attention + Wo
+	case 8: // fused attention + Wo (IPC: pushing exchange 0 of the bumped sequence, unread)
 		if constexpr (WT::BYTES <= 2)
-			return launch_attn_wo<WT>(d, w, l);
+			return launch_attn_wo<WT>(d, w, l, 0);
 		break;
 	}
 	set_err("bad kernel_id");
@@ -1346,7 +1369,7 @@ static int time_loop(yalm_decoder_s *d, int kernel_id, int iters, bool bump, boo
 	HIPCHK(hipEventRecord(e0, d->stream));
 	for (int i = 0; i < iters && r == YALM_OK; ++i) {
 		if (bump)
-			epoch_bump_kernel<<<1, 1, 0, d->stream>>>(d->step);
+			epoch_bump_kernel<<<1, 1, 0, d->stream>>>(d->step, 1);
 		// rotate layers so weights come from HBM, not the 256 MiB Infinity Cache
 		if (kernel)
 			r = DISPATCH_WT(d->c.weight_dtype, enqueue_one_t, d, kernel_id, (i + 1) % d->c.n_layers);
@@ -1366,7 +1389,8 @@ extern "C" int yalm_time_kernel(yalm_decoder d, int kernel_id, int iters, float 
 	       "bad argument (kernel ids 0-6, 8)");
 	ARGCHK(kernel_id != 6 || d->comm || d->ipc, "kernel 6 (tensor-parallel exchange) needs a tensor-parallel decoder");
 	ARGCHK(kernel_id != 8 || d->attn_wo, "kernel 8 (fused attention + Wo) needs yalm_decoder_attn_wo");
-	const bool bump = kernel_id == 1 || kernel_id == 8; // in-launch hand-offs: fresh tags per launch
+	// in-launch hand-offs and the IPC exchange: fresh tags per launch (one exchange per bump)
+	const bool bump = kernel_id == 1 || kernel_id == 8 || (kernel_id == 6 && d->ipc);
 	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_one_t, d, kernel_id, 0)); // warm-up
 	float ms = 0.f;
 	TRY(time_loop(d, kernel_id, iters, bump, true, &ms));

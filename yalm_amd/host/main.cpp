@@ -219,6 +219,10 @@ static void run_passkey(const std::string &path, const std::string &device, int 
 	const std::string PREFIX = "There is an important info hidden inside a lot of irrelevant text. "
 	                           "Find it and memorize them. I will quiz you about the important information there.";
 	const std::string SUFFIX = " What is the pass key? The pass key is";
+	// YALM_SEED (tests): re-seeded here, because the HIP runtime's initialisation above draws
+	// from std::rand too (two runs with the same seed otherwise got different passkeys)
+	if (getenv("YALM_SEED"))
+		std::srand((unsigned)sampler_seed());
 	const int passkey = std::rand() % 50000 + 1;
 	const int ppos = passkey_pos == -1 ? std::rand() % n_junk : passkey_pos;
 	std::string prompt = PREFIX;
@@ -233,6 +237,12 @@ static void run_passkey(const std::string &path, const std::string &device, int 
 	printf("Passkey test:\n  prompt: %zu tokens\n  passkey: %d\n  passkey token index: ~%d\n\n", encoding.size(),
 	       passkey, (int)(((float)ppos) / n_junk * encoding.size()));
 	const size_t N = encoding.size();
+	if (print_token_ids()) {
+		std::string pids;
+		for (int t : encoding)
+			pids += std::to_string(t) + " ";
+		fprintf(stderr, "PROMPT: %s\n", pids.c_str());
+	}
 	// the positions inside the context window before the last one in one batched prefill
 	// (yalm_prefill; the reference hydrates them one forward each, main.cpp:228-232); the
 	// rest -- past max_seq_len (sliding window + sinks) and the last prompt token, whose
@@ -247,6 +257,14 @@ static void run_passkey(const std::string &path, const std::string &device, int 
 		              pos + 1 == N ? InferenceMode::OUTPUT_LOGITS : InferenceMode::HYDRATE_KV_CACHE);
 	}
 	std::cout << std::endl << SUFFIX << std::flush;
+	if (const char *dump = getenv("YALM_DUMP_LOGITS")) { // test hook: the logits the answer starts from
+		FILE *f = fopen(dump, "wb");
+		if (!f || fwrite(state.logits(), sizeof(float), model.config->vocab_size, f) != (size_t)model.config->vocab_size) {
+			fprintf(stderr, "error: cannot write %s\n", dump);
+			exit(1);
+		}
+		fclose(f);
+	}
 	std::string ids;
 	for (size_t pos = N; pos < N + 16; ++pos) {
 		const int token = sampler.sample_argmax(state);
