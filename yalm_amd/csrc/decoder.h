@@ -139,6 +139,7 @@ struct yalm_decoder_s {
 	std::vector<void *> ipc_opened;  // hipIpcOpenMemHandle mappings to close
 	TpX tpx{};                       // the exchange descriptor passed to producers / consumers
 	bool tpx_gate = false;           // ranks share this GPU: a 1-wave wait launch before each consumer
+	bool tpx_collect = false;        // collect form (many ranks): a collect launch sums x before the consumer
 	// launch path: attention + Wo as one launch (attn_wo.h) when supported;
 	// YALM_ATTN_WO=0 selects the two separate kernels
 	bool attn_wo = false;

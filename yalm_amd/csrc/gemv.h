@@ -467,11 +467,12 @@ __global__ __launch_bounds__(GEMV_THREADS) void gemv_kernel(P p, const float *__
 // chunk (W1|W3 at n 4096: 8 reductions per row -> 1; tools/pattern_bench.hip: the chunk
 // order with its per-chunk work ran 10-25% below the streaming envelope, whole rows at it).
 //
-// TIN (tensor parallelism over IPC, tp_exchange.h): tin.n > 0 makes this launch the
-// consumer of an exchange -- x is the rank-order sum of every rank's pushed partial,
-// waited for and summed AFTER the first weight loads are issued, so the exchange latency
-// runs under the weight stream's start instead of in a launch of its own.
-template <class WT, class P, int U, bool NORM, int THREADS, bool ROWS = false>
+// TIN (tensor parallelism over IPC, tp_exchange.h): this launch is the consumer of exchange
+// tin -- x is the rank-order sum of every rank's pushed partial. The granules of the first
+// passes are loaded BEFORE the weight stream (as x is otherwise, XPre), waited for and summed
+// after it is issued, so the exchange latency runs under the weight stream's start instead
+// of in a launch of its own.
+template <class WT, class P, int U, bool NORM, int THREADS, bool ROWS = false, bool TIN = false>
 __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__restrict__ x,
                                                           const float *__restrict__ normw, float eps, TpX tin) {
 	extern __shared__ __attribute__((aligned(16))) float xs[];
@@ -519,11 +520,18 @@ __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__re
 
 	int ivr = ROWS ? wave : wave / nch, ic = ROWS ? 0 : wave - (wave / nch) * nch; // issue cursor
 	const int vr0 = ivr, c0 = ic;
-	const bool tpx = tin.n > 0;                                      // x from an exchange (uniform)
-	const bool xregs = !tpx && n <= 4 * xpre_n<NORM, THREADS>() * THREADS; // x (+ norm weights) fit the registers
+	const bool xregs = !TIN && n <= 4 * xpre_n<NORM, THREADS>() * THREADS; // x (+ norm weights) fit the registers
 	XPre<NORM, THREADS> xp;
-	if (xregs)
+	// exchange passes loaded ahead (n <= 4 * TPRE * THREADS: 4096 at 512 or 1024 threads)
+	constexpr int TPRE = TIN ? (THREADS >= 1024 ? 1 : 2) : 0;
+	TpxPre<TPRE ? TPRE : 1> tpre;
+	TpxView tview;
+	if constexpr (TIN) {
+		tview = tpx_view(tin, tin.g());
+		tpx_prefetch<NORM, THREADS, TPRE>(tpre, tview, tin, normw, n); // ahead of the weight stream in vmcnt order
+	} else if (xregs) {
 		prefetch_x<NORM, THREADS>(xp, x, normw, n); // ahead of the weight stream in vmcnt order
+	}
 	float xr[R] = {}; // PRE policies: the epilogue's rows of group threadIdx.x (clamped, unconditional)
 	if constexpr (gemv_pre<P>::value) {
 		const int g0 = min(b + min((int)threadIdx.x, max(ngl - 1, 0)) * NB, p.n_groups - 1);
@@ -540,8 +548,8 @@ __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__re
 	p.prologue();
 	for (int i = threadIdx.x; i < ngl * R * W; i += THREADS)
 		part[i] = 0.0f;
-	if (tpx)
-		tpx_stage_x<NORM>(xs, tin, tin.g(), normw, n, eps);
+	if constexpr (TIN)
+		tpx_stage_x<NORM, THREADS, TPRE>(xs, tin, tview, tpre, normw, n, eps);
 	else if (xregs)
 		stage_x_regs<NORM, THREADS>(xs, xp, n, eps);
 	else

@@ -204,18 +204,20 @@ __global__ __launch_bounds__(64) void tpx_gate_kernel(TpX t, int n) {
 }
 
 // Tensor parallelism over IPC: the consumer side of one exchange as a launch of its own --
-// the summed x into `out` (yalm_block's result; the timing hook of the exchange), or, with
-// gather, the n floats of every rank's slot side by side (the sharded logits).
-__global__ __launch_bounds__(1024) void tpx_collect_kernel(TpX t, int n, int gather, float *__restrict__ out) {
+// the summed x into `out` (the collect form of many ranks, yalm_block's result, the timing
+// hook), or, with gather, the n floats of every rank's slot side by side (the sharded
+// logits). Any grid: element i belongs to global thread i mod the grid's threads.
+__global__ __launch_bounds__(256) void tpx_collect_kernel(TpX t, int n, int gather, float *__restrict__ out) {
 	const unsigned g = t.g();
 	const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + TPX_TIMEOUT;
+	const int i0 = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
 	if (gather) {
 		for (int p = 0; p < t.n; ++p)
-			for (int i = threadIdx.x; i < n; i += blockDim.x)
+			for (int i = i0; i < n; i += stride)
 				out[(size_t)p * n + i] = tpx_get1(t, g, p, i, deadline);
 		return;
 	}
-	for (int i = threadIdx.x; i < n; i += blockDim.x) {
+	for (int i = i0; i < n; i += stride) {
 		float s = tpx_get1(t, g, 0, i, deadline);
 		for (int p = 1; p < t.n; ++p)
 			s += tpx_get1(t, g, p, i, deadline);

@@ -42,6 +42,13 @@
 
 #define TPX_TIMEOUT 200000000ull // 2 s of s_memrealtime (100 MHz)
 #define TPX_CTRL_WORDS 64        // error word + padding (in floats)
+// Consumer staging reads N x 32 KB of granules per workgroup (x of 4096): past this many ranks
+// a collect launch of TPX_COLLECT_WG workgroups sums x once instead (the collect form).
+// tools/tpx_stage_bench.hip, MI355X, 256 x 512-thread workgroups + a 29 MB weight stream (a
+// TP8 W1|W3): staging in the consumer 11.1 / 11.4 / 12.6 / 15.2 us at N = 1 / 2 / 4 / 8,
+// collect (32 workgroups) + plain staging 11.6 / 11.9 / 12.3 / 13.2, one GPU's plain 9.5.
+#define TPX_STAGE_MAX_RANKS 4
+#define TPX_COLLECT_WG 32
 
 struct TpX {
 	float *const *bufs;     // [n] this rank's buffer and the peers' (IPC-mapped), device array
@@ -84,63 +91,128 @@ __device__ __forceinline__ float tpx_get1(const TpX &t, unsigned g, int src, int
 	}
 }
 
-// Consumer: the summed x (rank order) of exchange g into LDS xs[0, n), optionally
-// rmsnorm'ed (infer.cpp:134-144, the statement order of stage_x), and workgroup 0 writes
-// the raw sum back to t.xw. Per pass a thread loads 4 elements of every rank (2 x 16-byte
-// sc0 sc1 loads of 2 granules each, through a buffer resource so the compiler tracks
-// them), all issued before any check; a pass re-reads until every tag in the wave is g + 1.
-template <bool NORM, int NMAX = 8>
-__device__ __forceinline__ void tpx_stage_x(float *xs, const TpX &t, unsigned g, const float *__restrict__ normw,
-                                            int n, float eps) {
-	const int tid = threadIdx.x, nthreads = blockDim.x;
+// Consumer view of exchange g in this rank's own buffer: a buffer resource over both
+// parities (a granule past the end reads as 0: tag 0 never matches), the parity's base.
+struct TpxView {
+	__amdgpu_buffer_rsrc_t own;
+	uint32_t base, rstride; // byte offset of slot [g & 1][0], bytes per source slot
+	unsigned tag;           // g + 1
+};
+
+__device__ __forceinline__ TpxView tpx_view(const TpX &t, unsigned g) {
+	TpxView w;
 	const uint64_t ba = (uint64_t)t.bufs[t.rank];
 	const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)ba), hi = __builtin_amdgcn_readfirstlane((uint32_t)(ba >> 32));
-	const __amdgpu_buffer_rsrc_t own = __builtin_amdgcn_make_buffer_rsrc(
-	    (void *)(((uint64_t)hi << 32) | lo), (short)0, (int)(2u * (uint32_t)t.n * (uint32_t)t.S * 8u), 0x00020000);
-	const uint32_t base = ((g & 1u) * (uint32_t)t.n) * (uint32_t)t.S * 8u, rstride = (uint32_t)t.S * 8u;
-	const unsigned tag = g + 1u;
+	w.own = __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0,
+	                                          (int)(2u * (uint32_t)t.n * (uint32_t)t.S * 8u), 0x00020000);
+	w.base = ((g & 1u) * (uint32_t)t.n) * (uint32_t)t.S * 8u;
+	w.rstride = (uint32_t)t.S * 8u;
+	w.tag = g + 1u;
+	return w;
+}
+
+// Elements [i, i + 4) of every source rank < nr: 2 x 16-byte sc0 sc1 loads (2 granules each)
+// per rank, all issued before any is used. Lanes with i >= n load nothing useful (an
+// out-of-range offset reads zeros) and are ignored by the check.
+template <int NMAX>
+__device__ __forceinline__ void tpx_load_pass(u32x4_t (&v)[NMAX][2], const TpxView &w, int nr, int i, int n) {
+#pragma unroll
+	for (int r = 0; r < NMAX; ++r)
+		if (r < nr) {
+			const uint32_t o = i < n ? w.base + (uint32_t)r * w.rstride + (uint32_t)i * 8u : 0x80000000u;
+			v[r][0] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(w.own, o, 0, 0x11));
+			v[r][1] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(w.own, o + 16u, 0, 0x11));
+		}
+}
+
+// Re-reads the pass until every tag in the wave is this exchange's (bounded: a give-up sets
+// the error word), then sums the ranks in rank order.
+template <int NMAX>
+__device__ __forceinline__ float4_t tpx_sum_pass(u32x4_t (&v)[NMAX][2], const TpxView &w, const TpX &t, int i, int n,
+                                                 unsigned long long deadline) {
+	for (;;) {
+		bool ok = true;
+#pragma unroll
+		for (int r = 0; r < NMAX; ++r)
+			if (r < t.n)
+				ok = ok && v[r][0][1] == w.tag && v[r][0][3] == w.tag && v[r][1][1] == w.tag && v[r][1][3] == w.tag;
+		if (__all(ok || i >= n))
+			break;
+		if (__builtin_amdgcn_s_memrealtime() > deadline) {
+			if ((threadIdx.x & 63) == 0)
+				__hip_atomic_store(t.err(), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+			break;
+		}
+		__builtin_amdgcn_s_sleep(1);
+		tpx_load_pass<NMAX>(v, w, t.n, i, n);
+	}
+	float4_t a;
+	{
+		const uint32_t e0 = v[0][0][0], e1 = v[0][0][2], e2 = v[0][1][0], e3 = v[0][1][2];
+		a = float4_t{__uint_as_float(e0), __uint_as_float(e1), __uint_as_float(e2), __uint_as_float(e3)};
+	}
+#pragma unroll
+	for (int r = 1; r < NMAX; ++r)
+		if (r < t.n) {
+			const uint32_t e0 = v[r][0][0], e1 = v[r][0][2], e2 = v[r][1][0], e3 = v[r][1][2];
+			a += float4_t{__uint_as_float(e0), __uint_as_float(e1), __uint_as_float(e2), __uint_as_float(e3)};
+		}
+	return a;
+}
+
+// The first PPRE passes of a consumer's x staging, loaded ahead of its weight stream (vmcnt
+// completes in order: granule loads issued behind the weight loads wait for them, and a
+// pass-by-pass loop serialised one uncached round trip per pass -- measured +1.8 / +2.0 us
+// per GLU / QKV launch at TP1). 8 VGPRs per rank slot (TPX_NMAX) and pass, plus the norm weights' 4 per pass.
+constexpr int TPX_NMAX = TPX_STAGE_MAX_RANKS;
+template <int PPRE>
+struct TpxPre {
+	u32x4_t v[PPRE][TPX_NMAX][2];
+	float4_t nw[PPRE];
+};
+
+template <bool NORM, int THREADS, int PPRE>
+__device__ __forceinline__ void tpx_prefetch(TpxPre<PPRE> &pre, const TpxView &w, const TpX &t,
+                                             const float *__restrict__ normw, int n) {
+#pragma unroll
+	for (int p = 0; p < PPRE; ++p)
+		if (p * THREADS * 4 < n) {
+			const int i = (p * THREADS + (int)threadIdx.x) * 4;
+			tpx_load_pass<TPX_NMAX>(pre.v[p], w, t.n, i, n);
+			if constexpr (NORM)
+				pre.nw[p] = *(const float4_t *)(normw + (i < n ? i : n - 4));
+		}
+}
+
+// Consumer: the summed x (rank order) of the exchange into LDS xs[0, n), optionally
+// rmsnorm'ed (infer.cu:526 / infer.cpp:134-144, the statement order of stage_x), and
+// workgroup 0 writes the raw sum back to t.xw. Passes past PPRE load here.
+template <bool NORM, int THREADS, int PPRE>
+__device__ __forceinline__ void tpx_stage_x(float *xs, const TpX &t, const TpxView &w, TpxPre<PPRE> &pre,
+                                            const float *__restrict__ normw, int n, float eps) {
+	const int tid = threadIdx.x;
 	const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + TPX_TIMEOUT;
 	float ss = 0.0f;
-	for (int i = tid * 4; i < n; i += nthreads * 4) {
-		u32x4_t v[NMAX][2];
-		for (;;) {
-#pragma unroll
-			for (int r = 0; r < NMAX; ++r)
-				if (r < t.n) {
-					const uint32_t o = base + (uint32_t)r * rstride + (uint32_t)i * 8u;
-					v[r][0] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(own, o, 0, 0x11));
-					v[r][1] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(own, o + 16u, 0, 0x11));
-				}
-			bool ok = true;
-#pragma unroll
-			for (int r = 0; r < NMAX; ++r)
-				if (r < t.n)
-					ok = ok && v[r][0][1] == tag && v[r][0][3] == tag && v[r][1][1] == tag && v[r][1][3] == tag;
-			if (__all(ok))
-				break;
-			if (__builtin_amdgcn_s_memrealtime() > deadline) {
-				if ((tid & 63) == 0)
-					__hip_atomic_store(t.err(), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-				break;
-			}
-			__builtin_amdgcn_s_sleep(1);
+	auto put = [&](int i, const float4_t &a) {
+		if (i < n) {
+			*(float4_t *)(xs + i) = a;
+			if (blockIdx.x == 0)
+				*(float4_t *)(t.xw + i) = a;
+			if constexpr (NORM)
+				ss = sumsq4(ss, a);
 		}
-		float4_t a;
-		{
-			const uint32_t e0 = v[0][0][0], e1 = v[0][0][2], e2 = v[0][1][0], e3 = v[0][1][2];
-			a = float4_t{__uint_as_float(e0), __uint_as_float(e1), __uint_as_float(e2), __uint_as_float(e3)};
-		}
+	};
 #pragma unroll
-		for (int r = 1; r < NMAX; ++r)
-			if (r < t.n) {
-				const uint32_t e0 = v[r][0][0], e1 = v[r][0][2], e2 = v[r][1][0], e3 = v[r][1][2];
-				a += float4_t{__uint_as_float(e0), __uint_as_float(e1), __uint_as_float(e2), __uint_as_float(e3)};
-			}
-		*(float4_t *)(xs + i) = a;
-		if (blockIdx.x == 0)
-			*(float4_t *)(t.xw + i) = a;
-		if constexpr (NORM)
-			ss = sumsq4(ss, a);
+	for (int p = 0; p < PPRE; ++p)
+		if (p * THREADS * 4 < n) {
+			const int i = (p * THREADS + tid) * 4;
+			put(i, tpx_sum_pass<TPX_NMAX>(pre.v[p], w, t, i, n, deadline));
+		}
+	for (int i0 = PPRE * THREADS * 4; i0 < n; i0 += THREADS * 4) {
+		const int i = i0 + tid * 4;
+		u32x4_t v[TPX_NMAX][2];
+		tpx_load_pass<TPX_NMAX>(v, w, t.n, i, n);
+		put(i, tpx_sum_pass<TPX_NMAX>(v, w, t, i, n, deadline));
 	}
 	if constexpr (NORM) {
 		float *red = xs + ((n + 3) & ~3);
@@ -149,18 +221,25 @@ __device__ __forceinline__ void tpx_stage_x(float *xs, const TpX &t, unsigned g,
 			red[tid >> 6] = ss;
 		__syncthreads();
 		float tot = 0.0f;
-		for (int w = 0; w < nthreads / YALM_WAVE; ++w)
-			tot += red[w];
+		for (int wv = 0; wv < THREADS / YALM_WAVE; ++wv)
+			tot += red[wv];
 		const float scale = 1.0f / sqrtf(tot / n + eps);
-		for (int i = tid * 4; i < n; i += nthreads * 4) {
+		auto norm = [&](int i, const float4_t &nw) {
 			float4_t v = *(const float4_t *)(xs + i);
-			const float4_t w = *(const float4_t *)(normw + i);
-			v[0] = v[0] * scale * w[0];
-			v[1] = v[1] * scale * w[1];
-			v[2] = v[2] * scale * w[2];
-			v[3] = v[3] * scale * w[3];
+			v[0] = v[0] * scale * nw[0];
+			v[1] = v[1] * scale * nw[1];
+			v[2] = v[2] * scale * nw[2];
+			v[3] = v[3] * scale * nw[3];
 			*(float4_t *)(xs + i) = v;
+		};
+#pragma unroll
+		for (int p = 0; p < PPRE; ++p) {
+			const int i = (p * THREADS + tid) * 4;
+			if (i < n)
+				norm(i, pre.nw[p]);
 		}
+		for (int i = (PPRE * THREADS + tid) * 4; i < n; i += THREADS * 4)
+			norm(i, *(const float4_t *)(normw + i));
 	}
 	__syncthreads();
 }

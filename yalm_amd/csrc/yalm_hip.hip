@@ -147,11 +147,33 @@ struct RowsMode<PQKV<WT>> {
 	static constexpr bool value = true;
 };
 
+// One launch of gemv_rb_kernel; a consumer of an IPC exchange (tin.n > 0, always a
+// normalising GEMV: QKV, W1|W3, logits) runs the TIN instantiation.
+template <class WT, class P, bool NORM, int THREADS, int U, bool ROWS>
+static int launch_rb_k(const P &p, const float *x, const float *normw, float eps, int nb, size_t lds, hipStream_t st,
+                       const TpX &tin) {
+	auto kern = gemv_rb_kernel<WT, P, U, NORM, THREADS, ROWS>;
+	if constexpr (NORM) {
+		if (tin.n > 0)
+			kern = gemv_rb_kernel<WT, P, U, NORM, THREADS, ROWS, true>;
+	} else if (tin.n > 0) {
+		set_err("internal: an exchange consumer must be a normalising GEMV");
+		return YALM_ERR_UNSUPPORTED;
+	}
+	if (lds > 65536)
+		HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+	hipLaunchKernelGGL(kern, dim3(nb), dim3(THREADS), lds, st, p, x, normw, eps, tin);
+	HIPCHK(hipGetLastError());
+	return YALM_OK;
+}
+
 template <class WT, class P, bool NORM, int THREADS, int U>
 static int launch_rb_t(const P &p, const float *x, const float *normw, float eps, int wpc, hipStream_t st,
                        const TpX &tin) {
-	const int nb = std::max(1, std::min(p.n_groups, device_cu_count() * std::max(1, wpc)));
+	// an exchange consumer stages x from the exchange once per CU: one workgroup per CU
+	const int nb = std::max(1, std::min(p.n_groups, device_cu_count() * (tin.n > 0 ? 1 : std::max(1, wpc))));
 	const int ngl = (p.n_groups + nb - 1) / nb;
+	const size_t lds = ((size_t)((p.n + 3) & ~3) + 64 + (size_t)ngl * P::R * (THREADS / YALM_WAVE)) * sizeof(float);
 	if constexpr (RowsMode<P>::value) {
 		// every workgroup the same number of rows and a whole number of rows, at least 2,
 		// per wave (profiles/r3_gemv_rows.txt: W1|W3 fp16 39.4-40.0 -> 36.9 us, fp8 W2 13.4 ->
@@ -159,24 +181,10 @@ static int launch_rb_t(const P &p, const float *x, const float *normw, float eps
 		// chunk order); YALM_GEMV_ROWS=0 keeps the chunk order everywhere (A/B)
 		const bool rows_on = !ab_env("YALM_GEMV_ROWS") || atoi(ab_env("YALM_GEMV_ROWS")) != 0;
 		constexpr int W = THREADS / YALM_WAVE;
-		if (rows_on && p.n_groups % nb == 0 && (ngl * P::R) % W == 0 && ngl * P::R >= 2 * W) {
-			auto kern = gemv_rb_kernel<WT, P, U, NORM, THREADS, true>;
-			const size_t lds =
-			    ((size_t)((p.n + 3) & ~3) + 64 + (size_t)ngl * P::R * (THREADS / YALM_WAVE)) * sizeof(float);
-			if (lds > 65536)
-				HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-			hipLaunchKernelGGL(kern, dim3(nb), dim3(THREADS), lds, st, p, x, normw, eps, tin);
-			HIPCHK(hipGetLastError());
-			return YALM_OK;
-		}
+		if (rows_on && p.n_groups % nb == 0 && (ngl * P::R) % W == 0 && ngl * P::R >= 2 * W)
+			return launch_rb_k<WT, P, NORM, THREADS, U, true>(p, x, normw, eps, nb, lds, st, tin);
 	}
-	auto kern = gemv_rb_kernel<WT, P, U, NORM, THREADS>;
-	const size_t lds = ((size_t)((p.n + 3) & ~3) + 64 + (size_t)ngl * P::R * (THREADS / YALM_WAVE)) * sizeof(float);
-	if (lds > 65536)
-		HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-	hipLaunchKernelGGL(kern, dim3(nb), dim3(THREADS), lds, st, p, x, normw, eps, tin);
-	HIPCHK(hipGetLastError());
-	return YALM_OK;
+	return launch_rb_k<WT, P, NORM, THREADS, U, false>(p, x, normw, eps, nb, lds, st, tin);
 }
 
 // Per-kind, per-weight-type defaults from tools/sweep_gemv.py on MI355X
@@ -565,7 +573,7 @@ static int launch_attn_wo(yalm_decoder_s *d, const yalm_block_weights &w, int la
 static int enqueue_exchange(yalm_decoder_s *d) {
 	if (d->ipc) {
 		tpx_push_kernel<<<1, 1024, 0, d->stream>>>(tpx_ex(d, 0), d->c.dim, d->x);
-		tpx_collect_kernel<<<1, 1024, 0, d->stream>>>(tpx_ex(d, 0), d->c.dim, 0, d->xs);
+		tpx_collect_kernel<<<TPX_COLLECT_WG, 256, 0, d->stream>>>(tpx_ex(d, 0), d->c.dim, 0, d->xs);
 		HIPCHK(hipGetLastError());
 		return YALM_OK;
 	}
@@ -632,12 +640,18 @@ static int enqueue_residual_gemv(yalm_decoder_s *d, const void *W, int n, const 
 	return YALM_OK;
 }
 
-// The exchange descriptor for a consumer launch. When this rank shares its GPU with a peer
-// (tests: several rank processes on one device), a 1-wave gate launch waits for the exchange
-// first: a consumer whose 256 workgroups spin in tpx_wait could otherwise hold every CU a
-// peer's producer needs (a deadlock the bounded wait only reports). One GPU per rank (the
-// real configuration) needs no gate: the consumer waits inside its own launch.
+// The exchange descriptor for a consumer launch (tp_exchange.h). Up to TPX_STAGE_MAX_RANKS
+// ranks every consumer workgroup sums the ranks' granules itself; past that a collect launch
+// sums x once and the consumer stages it as on one GPU (the collect form). When this rank
+// shares its GPU with a peer (tests: several rank processes on one device), a 1-wave gate
+// launch waits for the exchange first: a consumer whose 256 workgroups spin could otherwise
+// hold every CU a peer's producer needs (a deadlock the bounded wait only reports). One GPU
+// per rank (the real configuration) needs no gate: the consumer waits inside its own launch.
 static TpX tpx_consume(yalm_decoder_s *d, int ex, int n) {
+	if (d->tpx_collect) { // many ranks: x summed once by a collect launch, the consumer stages it as on one GPU
+		tpx_collect_kernel<<<TPX_COLLECT_WG, 256, 0, d->stream>>>(tpx_ex(d, ex), n, 0, d->x);
+		return TpX{};
+	}
 	if (d->tpx_gate)
 		tpx_gate_kernel<<<1, 64, 0, d->stream>>>(tpx_ex(d, ex), n);
 	return tpx_ex(d, ex);
@@ -763,7 +777,7 @@ static int enqueue_forward(yalm_decoder_s *d, int which) {
 	                d->ipc && which == GRAPH_LOGITS ? 2 * L : -1));
 	if (d->ipc) { // tp_exchange.h: no exchange launches
 		if (which == GRAPH_LOGITS) { // every rank's vocabulary slice, side by side
-			tpx_collect_kernel<<<1, 1024, 0, d->stream>>>(tpx_ex(d, 2 * L), d->c.vocab_size, 1, d->logits);
+			tpx_collect_kernel<<<TPX_COLLECT_WG, 256, 0, d->stream>>>(tpx_ex(d, 2 * L), d->c.vocab_size, 1, d->logits);
 			HIPCHK(hipGetLastError());
 			HIPCHK(hipMemcpyAsync(d->logits_pinned, d->logits, sizeof(float) * d->vocab_full, hipMemcpyDeviceToHost,
 			                      d->stream));
@@ -1113,6 +1127,7 @@ extern "C" int yalm_decoder_create_tp_ipc(const yalm_config *config, const yalm_
 	// out). Those ranks keep the separate attention and Wo launches.
 	if (d->tpx_gate && d->attn_wo && d->awo_nb * tp_size > d->awo_slots)
 		d->attn_wo = false;
+	d->tpx_collect = tp_size > TPX_STAGE_MAX_RANKS;
 	d->tpx.bufs = d->ipc_bufs;
 	d->tpx.rank = tp_rank;
 	d->tpx.n = tp_size;
@@ -1227,7 +1242,7 @@ extern "C" int yalm_block(yalm_decoder d, int layer, int pos, int kv_sink, int k
 	HIPCHK(hipGetLastError());
 	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_layer_t, d, layer, 0, false, true));
 	if (d->ipc) { // the layer's W2 pushed its partial: collect the sum into x (a forward's next GEMV would)
-		tpx_collect_kernel<<<1, 1024, 0, d->stream>>>(tpx_ex(d, 1), d->c.dim, 0, d->x);
+		tpx_collect_kernel<<<TPX_COLLECT_WG, 256, 0, d->stream>>>(tpx_ex(d, 1), d->c.dim, 0, d->x);
 		HIPCHK(hipGetLastError());
 	}
 	HIPCHK(hipStreamSynchronize(d->stream));
