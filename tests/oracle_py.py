@@ -122,13 +122,13 @@ def ffn(x, w1, w2, w3, act, dtype):
     return out
 
 
-def synth_host_tensors_fast(cfg: M.ModelConfig, seed: int = 1) -> dict:
+def synth_host_tensors_fast(cfg: M.ModelConfig, seed: int = 1, peak: float = 1.0) -> dict:
     """Full-size twin of DeviceModel.synthetic() built by the oracle's C
     initialiser (OpenMP): same hash, same bits."""
     out = {}
     for name, (shape, is_norm) in M.tensor_shapes(cfg).items():
         n = int(np.prod(shape))
-        scale, offset = M.synth_params(name, is_norm)
+        scale, offset = M.synth_params(name, is_norm, peak)
         s = M.synth_seed(seed, name)
         if is_norm:
             a = np.empty(n, np.float32)

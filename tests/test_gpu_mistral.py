@@ -48,31 +48,40 @@ def test_mistral_shape_greedy_parity(dtype):
         dm.close()
 
 
-def test_mistral_config2_256_tokens_vs_oracle():
+@pytest.mark.parametrize("peak", [1.0, M.PEAKED], ids=["uniform", "peaked"])
+def test_mistral_config2_256_tokens_vs_oracle(peak):
     """The config-2 workload as written (BASELINE.json: Mistral-7B fp16, all 32 layers,
     256 greedy tokens after the bench's 13-token prompt, kv_len up to 268) against the
     CPU oracle step by step: logits within 1e-3 rel at every step, the device's argmax
     equal to the oracle's wherever the oracle's top-2 margin exceeds 1e-3 of max|logit|
     (the sequence then continues with the device's token), and the device greedy loop
-    (one graph replay per token, argmax on the device) reproduces the sequence."""
+    (one graph replay per token, argmax on the device) reproduces the sequence.
+
+    peaked: the same model with the final norm weight x M.PEAKED, so the
+    next-token distributions are as peaked as a trained checkpoint's (top-1 probability
+    >= 0.5 at most steps, log ppl of the greedy text << ln(vocab)); the default synthetic
+    model's are near-uniform (logit std ~1.2)."""
     from yalm_amd import runtime
 
     cfg = M.MISTRAL_7B.with_(weight_dtype=M.F16)
-    dm = runtime.DeviceModel.synthetic(cfg, seed=1)
+    dm = runtime.DeviceModel.synthetic(cfg, seed=1, peak=peak)
     dec = runtime.Decoder(dm)
     dec2 = runtime.Decoder(dm)
     try:
-        om = O.OracleModel(cfg, O.synth_host_tensors_fast(cfg, seed=1))
+        om = O.OracleModel(cfg, O.synth_host_tensors_fast(cfg, seed=1, peak=peak))
         prompt = [(7 * i + 1) % cfg.vocab_size for i in range(13)]  # bench.py's prompt
         for pos, t in enumerate(prompt[:-1]):
             dec.forward(t, pos, runtime.HYDRATE_KV_CACHE)
             dec2.forward(t, pos, runtime.HYDRATE_KV_CACHE)
             om.forward(t, pos)
-        tok, pos, seq, near_ties, worst = prompt[-1], len(prompt) - 1, [], 0, 0.0
+        tok, pos, seq, near_ties, worst, p1, lp = prompt[-1], len(prompt) - 1, [], 0, 0.0, [], []
         for _ in range(256):
             lg = dec.forward(tok, pos).astype(np.float64)
             lo = om.forward(tok, pos).astype(np.float64)
             worst = max(worst, relerr(lg, lo))
+            lse = lo.max() + np.log(np.exp(lo - lo.max()).sum())
+            p1.append(float(np.exp(lo.max() - lse)))
+            lp.append(float(lo[int(np.argmax(lg))] - lse))
             assert relerr(lg, lo) < 1e-3, (pos, relerr(lg, lo))
             tg, to = int(np.argmax(lg)), int(np.argmax(lo))
             if tg != to:
@@ -81,8 +90,13 @@ def test_mistral_config2_256_tokens_vs_oracle():
                 near_ties += 1
             seq.append(tg)
             tok, pos = tg, pos + 1
-        print(f"256 tokens, kv_len {len(prompt)}..{pos}: worst logits rel {worst:.2e}, near-tie steps {near_ties}")
+        p1 = np.array(p1)
+        print(f"peak {peak}: 256 tokens, kv_len {len(prompt)}..{pos}: worst logits rel {worst:.2e}, near-tie steps "
+              f"{near_ties}; oracle top-1 probability median {np.median(p1):.3f}, >= 0.5 at {np.mean(p1 >= 0.5):.0%} "
+              f"of steps; log ppl of the greedy text {-np.mean(lp):.3f} (ln vocab {np.log(cfg.vocab_size):.2f})")
         assert near_ties <= 4
+        if peak > 1:
+            assert np.mean(p1 >= 0.5) >= 0.5 and -np.mean(lp) < 0.25 * np.log(cfg.vocab_size)
         dev = dec2.generate_greedy(prompt[-1], len(prompt) - 1, 256)
         assert list(dev) == seq
     finally:

@@ -42,8 +42,8 @@ def relerr(a, b):
     return float(np.max(np.abs(a - b)) / (np.max(np.abs(b)) + 1e-30))
 
 
-def kv_rows(cfg, seed):
-    """Per layer (K, V) [max_seq_len][kv_dim] f16: rows < HYDRATED seeded with the
+def kv_rows(cfg, seed, hydrated=HYDRATED):
+    """Per layer (K, V) [max_seq_len][kv_dim] f16: rows < hydrated seeded with the
     spread the model's own K/V have (std ~1.3 at this init), the rest zero."""
     rng = np.random.default_rng(seed)
     out = []
@@ -51,7 +51,7 @@ def kv_rows(cfg, seed):
         kv = []
         for _ in range(2):
             a = np.zeros((cfg.max_seq_len, cfg.kv_dim), np.float16)
-            a[:HYDRATED] = (rng.standard_normal((HYDRATED, cfg.kv_dim)) * 1.3).astype(np.float16)
+            a[:hydrated] = (rng.standard_normal((hydrated, cfg.kv_dim)) * 1.3).astype(np.float16)
             kv.append(a)
         out.append(kv)
     return out
@@ -60,9 +60,9 @@ def kv_rows(cfg, seed):
 class Pair:
     """Device decoder + oracle on the same weights and the same hydrated cache."""
 
-    def __init__(self, cfg, host, dm, kv_seed):
+    def __init__(self, cfg, host, dm, kv_seed, hydrated=HYDRATED):
         R = rt()
-        self.kv = kv_rows(cfg, kv_seed)
+        self.kv = kv_rows(cfg, kv_seed, hydrated)
         self.ptrs = []
         for k, v in self.kv:
             kp, vp = R.lib.yalm_upload(k.ctypes.data, k.nbytes), R.lib.yalm_upload(v.ctypes.data, v.nbytes)
@@ -109,6 +109,41 @@ def test_full_window_decode_into_sink_regime(model):
         assert p.dec.generate_greedy(tok, pos, 8) == p.om.greedy(tok, pos, 8)
     finally:
         p.close()
+
+
+def test_16k_window_decode_into_sink_regime(model):
+    """a -T 16384 window (model.cpp:31-36: the CLI's context override)
+    at Mistral dims, 2 layers: 256 64-key chunks per kv head, far past ATTN_MAX_SPLITS, so
+    every attention workgroup walks several chunks and the mergers fold many splits. Cache
+    rows 0 .. 16377 hydrated, then 16 positions decoded across max_seq_len into the sink
+    regime against the oracle, same bars as test_full_window_decode_into_sink_regime."""
+    cfg0, host, _ = model
+    if cfg0.weight_dtype != M.F16:
+        pytest.skip("the window length is independent of the weight type: f16 only")
+    cfg = cfg0.with_(max_seq_len=16384)
+    hyd = cfg.max_seq_len - 6
+    dm = rt().DeviceModel.synthetic(cfg, seed=3)
+    p = Pair(cfg, host, dm, kv_seed=13, hydrated=hyd)
+    worst = 0.0
+    try:
+        tok = 7
+        for pos in range(hyd, hyd + 16):  # kv_len 16379 .. 16384, then the ring + sinks
+            lg = p.dec.forward(tok, pos)
+            lo = p.om.forward(tok, pos)
+            e = relerr(lg, lo)
+            worst = max(worst, e)
+            assert e < 1e-3, (pos, e)
+            to = int(O.olib.orc_sample_argmax(O.P(lo), cfg.vocab_size))
+            srt = np.sort(lo)
+            if srt[-1] - srt[-2] > 1e-3 * np.max(np.abs(lo)):
+                assert int(np.argmax(lg)) == to, (pos, int(np.argmax(lg)), to)
+            tok = to
+        assert p.dec.generate_greedy(tok, hyd + 16, 8) == p.om.greedy(tok, hyd + 16, 8)
+        print(f"-T 16384, Mistral dims, 2 layers, fused attention + Wo {p.dec.attn_wo}: kv_len "
+              f"{hyd + 1}..{cfg.max_seq_len} then the sink regime, worst logits rel {worst:.2e}")
+    finally:
+        p.close()
+        dm.close()
 
 
 def test_per_layer_x_at_full_dims(model):

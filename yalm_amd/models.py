@@ -238,8 +238,18 @@ def synth_seed(base: int, name: str) -> int:
     return h
 
 
-def synth_params(name: str, is_norm: bool):
-    return (NORM_SCALE, NORM_OFFSET) if is_norm else (WEIGHT_SCALE, 0.0)
+def synth_params(name: str, is_norm: bool, peak: float = 1.0):
+    """(scale, offset) of a synthetic tensor. peak > 1 scales the final norm weight, so the
+    logits spread peak x wider: the default model's logits have a std of ~1.2 (near-uniform
+    next-token distributions), PEAKED's ~10 (top-1 probability >= 0.5 at most positions, as
+    trained checkpoints give)."""
+    if is_norm:
+        k = peak if name == "model.norm.weight" else 1.0
+        return NORM_SCALE * k, NORM_OFFSET * k
+    return WEIGHT_SCALE, 0.0
+
+
+PEAKED = 8.0  # synth_params(peak=PEAKED): the peaked synthetic models of the parity tests
 
 
 def _splitmix64(x):
@@ -267,12 +277,12 @@ def synth_array(n: int, dtype: int, seed: int, scale: float, offset: float = 0.0
     return ((hb + 0x7F + ((hb >> 8) & 1)) >> 8).astype(np.uint8)
 
 
-def synth_host_tensors(c: ModelConfig, seed: int = 1) -> dict:
+def synth_host_tensors(c: ModelConfig, seed: int = 1, peak: float = 1.0) -> dict:
     """All tensors of a synthetic model as numpy arrays (norms f32, weights in
     c.weight_dtype storage: f32 / f16 / uint8 E5M2 bits)."""
     out = {}
     for name, (shape, is_norm) in tensor_shapes(c).items():
-        scale, offset = synth_params(name, is_norm)
+        scale, offset = synth_params(name, is_norm, peak)
         dt = F32 if is_norm else c.weight_dtype
         n = int(np.prod(shape))
         out[name] = synth_array(n, dt, synth_seed(seed, name), scale, offset).reshape(shape)

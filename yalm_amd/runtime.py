@@ -301,7 +301,7 @@ class DeviceModel:
             yd.close()
 
     @classmethod
-    def synthetic(cls, cfg: M.ModelConfig, seed: int = 1, tp=(0, 1)) -> "DeviceModel":
+    def synthetic(cls, cfg: M.ModelConfig, seed: int = 1, tp=(0, 1), peak: float = 1.0) -> "DeviceModel":
         """Random-weight model of cfg's shape generated directly in HBM with the
         deterministic hash shared with the oracle (no PCIe upload). tp = (rank,
         size): keep only this rank's shards — each sharded tensor is generated
@@ -319,7 +319,7 @@ class DeviceModel:
             dt = M.F32 if is_norm else cfg.weight_dtype
             eb = M.DTYPE_BYTES[dt]
             src_name = "model.embed.weight" if name == "tp.wcls" else name
-            scale, offset = M.synth_params(src_name, is_norm)
+            scale, offset = M.synth_params(src_name, is_norm, peak)
             sh = M.tp_shard(cfg, name, rank, size)
             if sh is None:
                 p = self._alloc(n * eb)
