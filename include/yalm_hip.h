@@ -215,10 +215,15 @@ int yalm_decoder_create_tp(const yalm_config *config, const yalm_model_weights *
  * rank allocates its exchange buffer (yalm_tp_ipc_alloc, config = full model)
  * and shares the 64-byte hipIpcMemHandle out of band; every rank then passes
  * all tp_size handles (rank order; its own entry is ignored). The decoder
- * takes ownership of own_buf. Per exchange: the producer GEMV writes this
- * rank's partial into a slot of its buffer, then one kernel signals every peer
- * (system-scope flag stores), waits for theirs and sums (or gathers) all
- * ranks' slots in rank order, so results are identical on every rank. */
+ * takes ownership of own_buf (1..8 ranks). Per exchange no launch of its own:
+ * the producer (the fused attention + Wo launch, the W2 GEMV, the logits GEMV,
+ * the argmax) pushes each value of this rank's partial into this rank's slot of
+ * EVERY rank's buffer as an 8-byte {value, tag} granule (one system-scope store:
+ * the data is its own ready flag); the consumer (the next normalising GEMV)
+ * waits for every rank's granules while its weight stream starts and sums them
+ * in rank order, so x is identical on every rank. Past 4 ranks a collect launch
+ * sums x once before the consumer. The exchange sequence numbers live in the
+ * decoder's step state, so every rank must make the same calls in lockstep. */
 int yalm_tp_ipc_alloc(const yalm_config *config, int tp_size, void **buf, void *handle_out);
 int yalm_decoder_create_tp_ipc(const yalm_config *config, const yalm_model_weights *weights, int tp_rank, int tp_size,
                                void *own_buf, const void *handles, yalm_stream s, yalm_decoder *out);

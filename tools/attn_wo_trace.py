@@ -33,8 +33,12 @@ def main():
     dm = runtime.DeviceModel.synthetic(cfg, seed=1)
     dec = runtime.Decoder(dm)
     assert dec.attn_wo, "decoder does not run the fused attention + Wo launch"
-    for pos in range(args.ctx):
-        dec.forward((7 * pos + 1) % cfg.vocab_size, pos, runtime.HYDRATE_KV_CACHE)
+    toks = [(7 * pos + 1) % cfg.vocab_size for pos in range(args.ctx)]
+    if args.ctx > 64 and args.dtype == "fp16":  # long contexts: hydrate by the batched prefill
+        dec.prefill(toks, 0, logprobs=False)
+    else:
+        for pos, t in enumerate(toks):
+            dec.forward(t, pos, runtime.HYDRATE_KV_CACHE)
     dec.forward(5, args.ctx)
     tr, na = dec.attn_wo_trace()
     tr = tr.astype(np.int64)
