@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--model", default="mistral-7b")
     ap.add_argument("--ctx", type=int, default=150)
     ap.add_argument("--dtype", default="fp16", choices=["fp16", "fp8"])
+    ap.add_argument("--time", type=int, default=0, help="also time the fused launch (yalm_time_kernel 8), iterations")
     args = ap.parse_args()
     runtime.check(runtime.lib.yalm_set_device(0))
     cfg = M.PRESETS[args.model].with_(weight_dtype=M.F16 if args.dtype == "fp16" else M.F8E5M2)
@@ -41,6 +42,8 @@ def main():
             dec.forward(t, pos, runtime.HYDRATE_KV_CACHE)
     dec.forward(5, args.ctx)
     tr, na = dec.attn_wo_trace()
+    if args.time:
+        print(f"yalm_time_kernel(8) at kv_len {args.ctx + 1}: {dec.time_kernel(8, args.time) * 1e3:.2f} us")
     tr = tr.astype(np.int64)
     clk = tr[:, 8:]
     tr = tr[:, :8]
