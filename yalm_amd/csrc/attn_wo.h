@@ -41,10 +41,12 @@
 // at ONE column piece (256 / RPL threads per row).
 //
 // Outputs (round 5): x[row] = x + Wo v on one GPU; under tensor parallelism over RCCL
-// the partial (+ x on rank 0) goes to out = xs for the all-reduce; over IPC it is pushed
-// to every rank's exchange slot (tp_exchange.h) and the launch's last Wo workgroup bumps
-// the exchange count -- the attention + Wo launch IS the exchange's producer, and the
-// GLU GEMV after it the consumer.
+// the partial (+ x on rank 0) goes to out = xs for the all-reduce; over IPC each row is
+// pushed to every rank's exchange slot as a {value, tag} granule (tp_exchange.h) -- the
+// attention + Wo launch IS the exchange's producer, and the GLU GEMV after it the consumer.
+// (Round 5 measured a CU-paired workgroup order, attention units sharing CUs with attention
+// units and Wo with Wo, against this index order: the Wo stream from half the CUs lands
+// later and the launch lost 1.6-2.7 us at kv 31 / 4091, profiles/r5h_awo_cu_pairing_ab.txt.)
 #pragma once
 
 #include "attention.h"
