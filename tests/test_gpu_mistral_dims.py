@@ -203,9 +203,12 @@ def _tp_worker(rank, size, port, q):
 
 @pytest.mark.parametrize("size", [2, 4, 8])
 def test_tensor_parallel_ipc_mistral_dims_vs_oracle(size):
-    """TP over `size` processes on this GPU (IPC one-shot exchange; RCCL refuses
-    two ranks on one GPU) at Mistral dims: every rank's logits identical, and
-    equal to the CPU oracle's within 1e-3; greedy tokens identical to the oracle.
+    """TP over `size` processes on this GPU (the launch-lean IPC exchange, tp_exchange.h;
+    RCCL refuses two ranks on one GPU) at Mistral dims: every rank's logits identical,
+    and equal to the CPU oracle's within 1e-3; greedy tokens identical to the oracle.
+    Sizes 2 and 4 sum the exchanged x inside the consuming GEMVs; size 8 runs the
+    collect form (a collect launch before each consumer, TPX_STAGE_MAX_RANKS) and, with
+    8 fused grids unable to share one GPU, the separate attention and Wo launches.
     size 8 is the TP8 geometry of BASELINE config 5: per rank 1 kv head and 4 q
     heads (Wq 512 rows, Wk / Wv 128), Wo 512 columns, W1 / W3 1792 rows, W2 1792
     columns, a 4000-row vocabulary slice (argmax pick over 8 shards)."""
