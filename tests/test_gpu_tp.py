@@ -296,3 +296,67 @@ def test_tp_ipc_fused_launch_lean_multi_rank(size):
     finally:
         ref.close()
         dm.close()
+
+
+def _missing_peer_worker(rank, port, q):
+    import os
+    import time
+
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        from yalm_amd import runtime as R
+
+        dm = R.DeviceModel.synthetic(FUSED, seed=13, tp=(rank, 2))
+
+        def gather(h):
+            out = [None] * 2
+            dist.all_gather_object(out, h)
+            return out
+
+        dec = R.Decoder(dm, tp_gather=gather)
+        if rank == 0:  # rank 1 never runs a forward: every exchange of rank 0 waits for it
+            t0 = time.time()
+            err = ""
+            try:
+                dec.forward(5, 0)
+            except R.YalmError as e:
+                err = str(e)
+            q.put((time.time() - t0, err))
+        dist.barrier()  # rank 1 keeps its exchange buffer mapped until rank 0 is done
+        dec.close()
+        dm.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_tp_ipc_missing_peer_fails_fast():
+    """A rank whose peer never runs the forward: the first exchange wait gives up at its 2 s
+    deadline, every later wait of the same forward (2 L + 1 exchanges) gives up at once
+    (tp_exchange.h tpx_give_up), and the call reports it -- a broken transport costs one
+    timeout, not 2 s per exchange (bench.py then still reports the other transport)."""
+    import queue
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_missing_peer_worker, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        dt, err = q.get(timeout=240)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert "IPC exchange gave up" in err, err
+    assert 1.5 < dt < 2 * 2.0 + 2.0, dt  # one 2-s deadline (plus setup), not one per exchange

@@ -75,18 +75,29 @@ __device__ __forceinline__ void tpx_put(const TpX &t, unsigned g, int i, float v
 	}
 }
 
-// Consumer: one granule of source rank src (element i) of exchange g, waited for (bounded;
-// a wait that gives up sets the error word, reported by the next sync call).
+// A consumer's wait gives up at its deadline (2 s: the error word is set and reported by the
+// next sync call), or, after 10 us, as soon as an earlier wait of this rank has given up:
+// the results are invalid and reported already, and a forward of 2 L + 1 exchanges must not
+// spend 2 s on each of them (a failed transport on real xGMI then costs one timeout, not
+// minutes, and bench.py's other transport is still measured).
+__device__ __forceinline__ bool tpx_give_up(const TpX &t, unsigned long long deadline) {
+	const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+	if (now > deadline) {
+		__hip_atomic_store(t.err(), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+		return true;
+	}
+	return now + TPX_TIMEOUT > deadline + 1000ull &&
+	       __hip_atomic_load(t.err(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
+}
+
+// Consumer: one granule of source rank src (element i) of exchange g, waited for (bounded,
+// tpx_give_up).
 __device__ __forceinline__ float tpx_get1(const TpX &t, unsigned g, int src, int i, unsigned long long deadline) {
 	const unsigned long long *s = t.slot(t.rank, g, src) + i;
 	for (;;) {
 		const unsigned long long v = __hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-		if ((unsigned)(v >> 32) == g + 1u)
+		if ((unsigned)(v >> 32) == g + 1u || tpx_give_up(t, deadline))
 			return __uint_as_float((unsigned)v);
-		if (__builtin_amdgcn_s_memrealtime() > deadline) {
-			__hip_atomic_store(t.err(), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-			return __uint_as_float((unsigned)v);
-		}
 		__builtin_amdgcn_s_sleep(1);
 	}
 }
@@ -138,11 +149,8 @@ __device__ __forceinline__ float4_t tpx_sum_pass(u32x4_t (&v)[NMAX][2], const Tp
 				ok = ok && v[r][0][1] == w.tag && v[r][0][3] == w.tag && v[r][1][1] == w.tag && v[r][1][3] == w.tag;
 		if (__all(ok || i >= n))
 			break;
-		if (__builtin_amdgcn_s_memrealtime() > deadline) {
-			if ((threadIdx.x & 63) == 0)
-				__hip_atomic_store(t.err(), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+		if (__any(tpx_give_up(t, deadline))) // (wave-uniform exit)
 			break;
-		}
 		__builtin_amdgcn_s_sleep(1);
 		tpx_load_pass<NMAX>(v, w, t.n, i, n);
 	}
