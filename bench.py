@@ -491,8 +491,12 @@ def main():
         import torch.distributed as dist_mod
 
         # host-side control only (unique id, barriers, max-over-ranks time): gloo;
-        # the data path is the decoder's own RCCL communicator / IPC exchange
-        dist_mod.init_process_group("gloo")
+        # the data path is the decoder's own RCCL communicator / IPC exchange. A 300-s
+        # timeout (default 30 min): if a transport fails on some ranks only, the others'
+        # barriers raise (caught like the failure itself) instead of stalling the run
+        import datetime
+
+        dist_mod.init_process_group("gloo", timeout=datetime.timedelta(seconds=300))
         dist = dist_mod
 
     profiled = any(k.startswith("ROCPROF") for k in os.environ)
