@@ -687,7 +687,21 @@ def main():
         # the same workload through the IPC one-shot exchange (include/yalm_hip.h), for
         # the all-reduce cost of RCCL's collective vs direct peer-mapped stores
         try:
-            dm, dec = make_decoder(runtime, M, cfg, rank, world, "tp-ipc", dist)
+            # every rank learns whether the IPC decoder came up everywhere before any rank
+            # enters the timed decode (a rank that failed alone would otherwise meet the
+            # others' barriers out of step)
+            ok2, err2 = 1, None
+            try:
+                dm, dec = make_decoder(runtime, M, cfg, rank, world, "tp-ipc", dist)
+            except Exception as e:
+                ok2, err2 = 0, e
+            oks2 = [None] * world
+            dist.all_gather_object(oks2, ok2)
+            if not all(oks2):
+                if ok2:
+                    dec.close()
+                    dm.close()
+                raise err2 or RuntimeError("the IPC decoder failed on another rank")
             e2, _, _, agree2 = timed_decode(dec, True)
             k2 = graph_kernels(dec)
             ex2 = dec.time_kernel(6, args.kernel_iters) * 1e3
