@@ -7,6 +7,7 @@ set -e
 rev=$1
 def=""; suf=""
 if [ "$2" = "ab" ]; then def="-DYALM_AB"; suf="_ab"; fi
+[ -n "${AB_SUFFIX:-}" ] && suf="${suf}_${AB_SUFFIX}"
 root=$(cd "$(dirname "$0")/.." && pwd)
 tmp=$(mktemp -d)
 if [ "$rev" = wt ]; then  # the working tree
@@ -15,9 +16,9 @@ else
   git -C "$root" archive "$rev" yalm_amd/csrc include | tar -x -C "$tmp"
 fi
 mkdir -p "$root/yalm_amd/ab"
-for f in yalm_hip prefill; do
+for f in yalm_hip prefill; do  # EXTRA_DEFS: more -D flags for the A/B build
   extra=""; [ $f = prefill ] && extra="-mllvm -amdgpu-mfma-vgpr-form"
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $def $extra -c -o "$tmp/$f.o" "$tmp/yalm_amd/csrc/$f.hip" &
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $def ${EXTRA_DEFS:-} $extra -c -o "$tmp/$f.o" "$tmp/yalm_amd/csrc/$f.hip" &
 done
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -o "$root/yalm_amd/ab/libyalm_hip_$rev$suf.so" \
