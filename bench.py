@@ -514,35 +514,20 @@ def main():
     cfg = base.with_(weight_dtype=M.F16 if args.dtype == "fp16" else M.F8E5M2)
 
     if world == 1:
-        mode = f"tp-{args.tp_transport}" if args.tp else "single"
+        first = f"tp-{args.tp_transport}" if args.tp else "single"
+        candidates = [first] + (["single"] if first != "single" else [])
     else:
-        mode = "replica" if args.replicas else f"tp-{args.tp_transport}"
-    fallback = None
-    try:
-        dm, dec = make_decoder(runtime, M, cfg, rank, world, mode, dist)
-        ok = 1
-    except Exception as e:  # a transport that cannot come up on this node: say so, then fall back
-        fallback = f"{mode} failed on rank {rank}: {str(e)[:200]}"
-        ok = 0
-    if dist is not None:
+        first = "replica" if args.replicas else f"tp-{args.tp_transport}"
+        # a transport that cannot come up (or cannot decode) on this node: the other
+        # transport, then independent replicas; every rank takes the same decision
+        candidates = [first] + (["tp-ipc"] if first == "tp-rccl" else []) + (["replica"] if first != "replica" else [])
+
+    def all_ok(ok):
+        if dist is None:
+            return ok
         oks = [None] * world
         dist.all_gather_object(oks, ok)
-        if not all(oks) and ok:
-            dec.close()
-            dm.close()
-            fallback = fallback or f"{mode} failed on another rank"
-            ok = 0
-    if not ok:
-        mode = "replica" if world > 1 else "single"
-        dm, dec = make_decoder(runtime, M, cfg, rank, world, mode, dist)
-    tp = mode.startswith("tp-")
-    tp_size = world if tp else 1
-    if args.long_only:
-        print(json.dumps(long_context_leg(runtime, M, cfg, dm, steps=args.long_steps,
-                                          kernel_iters=args.kernel_iters)), file=real_stdout, flush=True)
-        dec.close()
-        dm.close()
-        return
+        return all(oks)
 
     def timed_decode(dec, tp):
         """Hydrate the prompt, warm up, then time exactly args.steps greedy tokens
@@ -587,7 +572,43 @@ def main():
                 agree = len({(v[1], v[2]) for v in allv}) == 1
         return elapsed, pos0, pos1, agree
 
-    elapsed, pos0, pos1, agree = timed_decode(dec, tp)
+    fallback = None
+    result = None
+    for mode in candidates:
+        dm = dec = None
+        err = None
+        try:
+            dm, dec = make_decoder(runtime, M, cfg, rank, world, mode, dist)
+        except Exception as e:
+            err = f"{mode} failed on rank {rank}: {str(e)[:200]}"
+        ok = all_ok(err is None)
+        if ok and not args.long_only:
+            try:
+                result = timed_decode(dec, mode.startswith("tp-"))
+            except Exception as e:
+                err = f"{mode} decode failed on rank {rank}: {str(e)[:200]}"
+            ok = all_ok(err is None)
+        if ok:
+            break
+        fallback = (fallback + "; " if fallback else "") + (err or f"{mode} failed on another rank")
+        for h in (dec, dm):
+            if h is not None:
+                try:
+                    h.close()
+                except Exception:
+                    pass
+        if mode == candidates[-1]:
+            raise RuntimeError(fallback)
+    tp = mode.startswith("tp-")
+    tp_size = world if tp else 1
+    if args.long_only:
+        print(json.dumps(long_context_leg(runtime, M, cfg, dm, steps=args.long_steps,
+                                          kernel_iters=args.kernel_iters)), file=real_stdout, flush=True)
+        dec.close()
+        dm.close()
+        return
+
+    elapsed, pos0, pos1, agree = result
 
     # ---- roofline of the dominant kernel: the W1/W3 GEMV + SiLU-GLU (52.9% of the bytes)
     wb = M.DTYPE_BYTES[cfg.weight_dtype]
