@@ -9,7 +9,7 @@ k | v columns only), R2 Q, R3 P in attention,
 R4 the attention output O (Wo's A operand), R5 the GLU A operand, R6 the GLU
 output H (W2's A operand), R7 the classifier's A operand.
 
-usage: python tools/prefill_precision_emul.py [--layers 2] [--n 128]
+usage: python tools/prefill_precision_emul.py [--layers 2] [--n 128] [--peak 8]
 """
 import argparse
 import os
@@ -104,14 +104,15 @@ def main():
     ap.add_argument("--n", type=int, default=128)
     ap.add_argument("--seed", type=int, default=6, help="synthetic weight seed")
     ap.add_argument("--tokseed", type=int, default=-1, help="token rng seed (default 1000 + layers)")
+    ap.add_argument("--peak", type=float, default=1.0, help="final-norm scale (models.PEAKED = 8: a trained checkpoint's logit spread)")
     ap.add_argument("--sets", default="", help="comma-separated rounding sets to run, e.g. 'R1+R2,all-R1' (default: each alone, then all)")
     args = ap.parse_args()
     cfg = M.LLAMA_32_3B.with_(n_layers=args.layers, max_seq_len=max(args.n, 64))
-    t = O.synth_host_tensors_fast(cfg, seed=args.seed)
+    t = O.synth_host_tensors_fast(cfg, seed=args.seed, peak=args.peak)
     tseed = args.tokseed if args.tokseed >= 0 else 1000 + args.layers
     tokens = np.random.default_rng(tseed).integers(0, cfg.vocab_size, size=args.n)
     base = run(cfg, t, tokens, set())
-    print(f"llama-3b dims, {args.layers} layers, {args.n} positions; log ppl {-base.mean():.4f}")
+    print(f"llama-3b dims, {args.layers} layers, {args.n} positions, peak {args.peak}; log ppl {-base.mean():.4f}")
     allr = {"R1", "R2", "R3", "R4", "R5", "R6", "R7"}
     sets = [{"R1"}, {"R2"}, {"R3"}, {"R4"}, {"R5"}, {"R6"}, {"R7"}, allr]
     if args.sets:
@@ -127,7 +128,7 @@ def main():
         lp = run(cfg, t, tokens, R)
         d = np.abs(lp - base)
         print(f"  {'+'.join(sorted(R)):24s} max |d log p| {d.max():.2e}  p99 {np.quantile(d, 0.99):.2e}  "
-              f"median {np.median(d):.2e}", flush=True)
+              f"median {np.median(d):.2e}  |d log ppl| {abs(lp.mean() - base.mean()):.2e}", flush=True)
 
 
 if __name__ == "__main__":
