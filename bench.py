@@ -429,6 +429,18 @@ def tp_info(mode, exch_us, kernels, cfg, agree):
     return out
 
 
+def transport_candidates(world, tp, transport, replicas):
+    """Decoder modes bench.py tries in order: the requested one, then (N > 1) the other
+    tensor-parallel transport after RCCL, then independent replicas (N = 1: one GPU).
+    A mode that cannot come up, or whose timed decode raises, on any rank moves every
+    rank to the next."""
+    if world == 1:
+        first = f"tp-{transport}" if tp else "single"
+        return [first] + (["single"] if first != "single" else [])
+    first = "replica" if replicas else f"tp-{transport}"
+    return [first] + (["tp-ipc"] if first == "tp-rccl" else []) + (["replica"] if first != "replica" else [])
+
+
 def make_decoder(runtime, M, cfg, rank, world, mode, dist):
     """(DeviceModel, Decoder) for mode "single" | "replica" | "tp-rccl" | "tp-ipc"."""
     if mode in ("single", "replica"):
@@ -513,14 +525,7 @@ def main():
     base = M.PRESETS[args.model]
     cfg = base.with_(weight_dtype=M.F16 if args.dtype == "fp16" else M.F8E5M2)
 
-    if world == 1:
-        first = f"tp-{args.tp_transport}" if args.tp else "single"
-        candidates = [first] + (["single"] if first != "single" else [])
-    else:
-        first = "replica" if args.replicas else f"tp-{args.tp_transport}"
-        # a transport that cannot come up (or cannot decode) on this node: the other
-        # transport, then independent replicas; every rank takes the same decision
-        candidates = [first] + (["tp-ipc"] if first == "tp-rccl" else []) + (["replica"] if first != "replica" else [])
+    candidates = transport_candidates(world, args.tp, args.tp_transport, args.replicas)
 
     def all_ok(ok):
         if dist is None:
