@@ -116,6 +116,11 @@ struct yalm_decoder_s {
 	long long host_pos = -1;         // position of the next forward as the host knows it (-1: unknown)
 	GemvCfg gemv[GK_N];
 	bool eager = false;     // YALM_EAGER=1: launch kernels directly (profilers that mis-handle graph replay)
+	// the device greedy loop (yalm_enqueue_greedy / yalm_generate_greedy) launches its forwards
+	// directly rather than replaying GRAPH_GREEDY: measured 0.6-1.1% faster on MI355X in six
+	// interleaved rounds (profiles/r5y_graph_vs_eager.txt); the host issues the 131 launches of
+	// a token well inside the token's 1.6-2.5 ms. A/B builds: YALM_GREEDY_GRAPH=1 replays.
+	bool greedy_eager = true;
 	bool graph_sync = false; // YALM_GRAPH_SYNC=1: synchronise after every replay
 	std::string kname;
 	PrefillBufs pf;

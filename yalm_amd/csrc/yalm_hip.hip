@@ -883,7 +883,7 @@ int dalloc(yalm_decoder_s *d, void **p, size_t bytes) {
 // One forward of graph `which`: a graph replay, or the same kernels launched
 // eagerly when d->eager.
 static int replay(yalm_decoder_s *d, int which) {
-	if (d->eager)
+	if (d->eager || (which == GRAPH_GREEDY && d->greedy_eager))
 		return enqueue_forward(d, which);
 	HIPCHK(hipGraphLaunch(d->exec[which], d->stream));
 	if (d->graph_sync)
@@ -928,6 +928,10 @@ static int create_decoder(const yalm_config *config, const yalm_model_weights *w
 	d->pf_forms = pf_forms_default();
 	d->eager = getenv("YALM_EAGER") && atoi(getenv("YALM_EAGER")) != 0;
 	d->graph_sync = getenv("YALM_GRAPH_SYNC") && atoi(getenv("YALM_GRAPH_SYNC")) != 0;
+	{
+		const char *g = ab_env("YALM_GREEDY_GRAPH");
+		d->greedy_eager = !(g && atoi(g) != 0);
+	}
 	// geometry overrides for A/B runs without a rebuild (same meaning as yalm_set_gemv_config):
 	// YALM_GEMV_CFG="kind:threads:unroll:gpw[,kind:threads:unroll:gpw...]", kind 0..4
 	if (const char *g = ab_env("YALM_GEMV_CFG")) {
@@ -1174,7 +1178,8 @@ extern "C" int yalm_forward(yalm_decoder d, int token, int pos, int mode, float 
 
 extern "C" int yalm_enqueue_greedy(yalm_decoder d, int n_steps) {
 	ARGCHK(d, "null decoder");
-	TRY(ensure_graph(d, GRAPH_GREEDY));
+	if (!d->greedy_eager)
+		TRY(ensure_graph(d, GRAPH_GREEDY));
 	for (int i = 0; i < n_steps; ++i) { // each replay advances the device position by one
 		TRY(replay(d, GRAPH_GREEDY));
 		if (d->host_pos >= 0)
@@ -1186,7 +1191,8 @@ extern "C" int yalm_enqueue_greedy(yalm_decoder d, int n_steps) {
 extern "C" int yalm_generate_greedy(yalm_decoder d, int token, int pos, int n_steps, int *out_tokens) {
 	ARGCHK(d && out_tokens, "null argument");
 	ARGCHK(token >= 0 && token < d->vocab_full && pos >= 0 && n_steps >= 0, "bad token/pos/n_steps");
-	TRY(ensure_graph(d, GRAPH_GREEDY));
+	if (!d->greedy_eager)
+		TRY(ensure_graph(d, GRAPH_GREEDY));
 	int done = 0;
 	bool first = true;
 	while (done < n_steps) {
