@@ -56,6 +56,7 @@
 #define AWO_RPW 16                   // Wo rows per Wo workgroup (256 of them for Mistral-7B)
 #define AWO_TIMEOUT 200000000ull     // 2 s of s_memrealtime (100 MHz)
 #define AWO_REPL_STRIDE 32           // words of the error slot (a 128-B line of its own)
+#define AWO_SHORT_KV 64             // kv_len up to which fp8 decoders start the Wo slice loads at once (decoder.h)
 #define AWO_TRACE_N 16               // s_memrealtime + s_memtime stamps per workgroup (yalm_attn_wo_trace)
 
 struct AttnWoArgs {

@@ -153,6 +153,13 @@ struct yalm_decoder_s {
 	int awo_slots = 0;               // co-resident workgroup slots of the fused launch (occupancy x CUs)
 	unsigned long long *awo_trace = nullptr; // A/B build, YALM_ATTN_WO_TRACE=1: [grid][16] stamps of the last launch
 	int awo_delay = 0;               // ticks the Wo workgroups wait before their slice loads
+	// fp8 at kv_len <= AWO_SHORT_KV: no wait (round 5 sweep, profiles/r5aa_awo_delay_short.txt:
+	// kv 17 / 32 / 64 7.72 / 7.43 / 7.56 us against 8.18 / 8.07 / 8.12 at 0.5 us, while kv 151 /
+	// 401 keep the 0.5 us). The eager greedy loop knows each forward's kv_len from the host-side
+	// position (awo_kv_hint); graph captures and unknown positions use awo_delay. A wrong hint
+	// changes only the timing.
+	int awo_delay_short = -1;        // -1: same as awo_delay
+	long long awo_kv_hint = -1;      // kv_len of the forward being enqueued, -1 unknown
 	unsigned long long *awo_gran = nullptr; // [n_layers][q_dim] attention outputs as {value, epoch} granules
 	unsigned *awo_err = nullptr;     // error word of the in-launch waits (bit 0 fused Wo gather, bit 1 attention merger)
 };

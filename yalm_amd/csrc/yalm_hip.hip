@@ -447,6 +447,7 @@ static int attn_wo_init(yalm_decoder_s *d) {
 	// ~3.1 us, before the heads): 0.5 us gives 9.4 -> 8.4 us at kv 17, 11.3 -> 10.3 at kv 151,
 	// 579 -> 586 tok/s (profiles/r3_ab_awo_delay.txt); fp16 at 0.5 us is within noise
 	d->awo_delay = denv ? std::max(0, atoi(denv)) : (c.weight_dtype == YALM_F8E5M2 ? 50 : 20);
+	d->awo_delay_short = denv ? -1 : (c.weight_dtype == YALM_F8E5M2 ? 0 : -1);
 	// Removed in round 4 (measured losers, round 3, profiles/r3_ab_awo*.txt): the combined
 	// first gather attempt (YALM_AWO_SPEC), per-XCD copies of the head outputs
 	// (YALM_AWO_REPL) and a sliding window on the Wo slice loads (YALM_ATTN_WO_WIN)
@@ -541,7 +542,8 @@ static int launch_attn_wo(yalm_decoder_s *d, const yalm_block_weights &w, int la
 	p.push = d->ipc ? tpx_ex(d, ex) : TpX{};
 	p.err = d->awo_err;
 	p.trace = d->awo_trace;
-	p.delay = d->awo_delay;
+	p.delay = d->awo_delay_short >= 0 && d->awo_kv_hint >= 0 && d->awo_kv_hint <= AWO_SHORT_KV ? d->awo_delay_short
+	                                                                                         : d->awo_delay;
 	const int G = c.n_heads / c.n_kv_heads;
 	if constexpr (WT::BYTES == 2 || WT::BYTES == 1) {
 		switch (p.q_dim * WT::BYTES) {
@@ -1176,23 +1178,32 @@ extern "C" int yalm_forward(yalm_decoder d, int token, int pos, int mode, float 
 	return YALM_OK;
 }
 
-extern "C" int yalm_enqueue_greedy(yalm_decoder d, int n_steps) {
-	ARGCHK(d, "null decoder");
+// n greedy forwards from position pos0 (-1: unknown); the eager path passes each forward's
+// kv_len to the attention + Wo launch (awo_kv_hint), graph replays cannot
+static int replay_greedy(yalm_decoder_s *d, int n, long long pos0) {
 	if (!d->greedy_eager)
 		TRY(ensure_graph(d, GRAPH_GREEDY));
-	for (int i = 0; i < n_steps; ++i) { // each replay advances the device position by one
-		TRY(replay(d, GRAPH_GREEDY));
-		if (d->host_pos >= 0)
-			++d->host_pos;
+	int r = YALM_OK;
+	for (int i = 0; i < n && r == YALM_OK; ++i) {
+		d->awo_kv_hint = pos0 >= 0 ? std::min<long long>(pos0 + i + 1, d->c.max_seq_len) : -1;
+		r = replay(d, GRAPH_GREEDY);
 	}
+	d->awo_kv_hint = -1;
+	return r;
+}
+
+extern "C" int yalm_enqueue_greedy(yalm_decoder d, int n_steps) {
+	ARGCHK(d, "null decoder");
+	ARGCHK(n_steps >= 0, "bad n_steps");
+	TRY(replay_greedy(d, n_steps, d->host_pos)); // each forward advances the device position by one
+	if (d->host_pos >= 0)
+		d->host_pos += n_steps;
 	return YALM_OK;
 }
 
 extern "C" int yalm_generate_greedy(yalm_decoder d, int token, int pos, int n_steps, int *out_tokens) {
 	ARGCHK(d && out_tokens, "null argument");
 	ARGCHK(token >= 0 && token < d->vocab_full && pos >= 0 && n_steps >= 0, "bad token/pos/n_steps");
-	if (!d->greedy_eager)
-		TRY(ensure_graph(d, GRAPH_GREEDY));
 	int done = 0;
 	bool first = true;
 	while (done < n_steps) {
@@ -1203,8 +1214,7 @@ extern "C" int yalm_generate_greedy(yalm_decoder d, int token, int pos, int n_st
 			set_step_kernel<<<1, 1, 0, d->stream>>>(d->step, out_tokens[done - 1], pos + done, 1);
 		HIPCHK(hipGetLastError());
 		first = false;
-		for (int i = 0; i < batch; ++i)
-			TRY(replay(d, GRAPH_GREEDY));
+		TRY(replay_greedy(d, batch, (long long)pos + done));
 		d->host_pos = (long long)pos + done + batch;
 		HIPCHK(hipMemcpyAsync(out_tokens + done, d->tokens, sizeof(int) * batch, hipMemcpyDeviceToHost, d->stream));
 		HIPCHK(hipStreamSynchronize(d->stream));
