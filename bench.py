@@ -68,6 +68,12 @@ def parse():
                     help="N > 1 over RCCL: skip the second measurement through the IPC exchange")
     ap.add_argument("--no-gpu-state", action="store_true",
                     help="skip the rocm-smi query (under a profiler: its preload would run inside rocm-smi too)")
+    ap.add_argument("--eager", action="store_true",
+                    help="single forwards launch their kernels directly instead of replaying graphs (profilers)")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="N > 1 on ONE GPU: every rank on device 0, its decoder stream on a disjoint block of "
+                         "256/N CUs (yalm_stream_create_cu_part), IPC transport -- config 5's production launch "
+                         "sequence rehearsed, not a scaling measurement")
     return ap.parse_args()
 
 
@@ -406,7 +412,7 @@ def tp_bytes_per_token(cfg, size):
 
 def graph_kernels(dec):
     """Kernel launches per greedy token (the captured graph's kernel nodes); None when the
-    decoder launches eagerly (YALM_EAGER=1 under the profiler)."""
+    decoder launches eagerly (--eager under the profiler)."""
     try:
         return dec.graph_kernels(2)
     except Exception:
@@ -441,11 +447,12 @@ def transport_candidates(world, tp, transport, replicas):
     return [first] + (["tp-ipc"] if first == "tp-rccl" else []) + (["replica"] if first != "replica" else [])
 
 
-def make_decoder(runtime, M, cfg, rank, world, mode, dist):
-    """(DeviceModel, Decoder) for mode "single" | "replica" | "tp-rccl" | "tp-ipc"."""
+def make_decoder(runtime, M, cfg, rank, world, mode, dist, launch=0, cu_part=None):
+    """(DeviceModel, Decoder) for mode "single" | "replica" | "tp-rccl" | "tp-ipc"; cu_part:
+    the decoder stream's CU block (the one-GPU rehearsal)."""
     if mode in ("single", "replica"):
         dm = runtime.DeviceModel.synthetic(cfg, seed=1)
-        return dm, runtime.Decoder(dm)
+        return dm, runtime.Decoder(dm, launch=launch, cu_part=cu_part)
     dm = runtime.DeviceModel.synthetic(cfg, seed=1, tp=(rank, world))
     if mode == "tp-ipc":
         def gather(h):
@@ -453,11 +460,12 @@ def make_decoder(runtime, M, cfg, rank, world, mode, dist):
             dist.all_gather_object(out, h)
             return out
 
-        return dm, runtime.Decoder(dm, tp_gather=gather if world > 1 else (lambda h: [h]))
+        return dm, runtime.Decoder(dm, tp_gather=gather if world > 1 else (lambda h: [h]), launch=launch,
+                                   cu_part=cu_part)
     uid = [runtime.tp_unique_id() if rank == 0 else None]
     if world > 1:
         dist.broadcast_object_list(uid, src=0)
-    return dm, runtime.Decoder(dm, tp_id=uid[0])
+    return dm, runtime.Decoder(dm, tp_id=uid[0], launch=launch, cu_part=cu_part)
 
 
 def fp8_leg(args):
@@ -519,20 +527,27 @@ def main():
     from yalm_amd import models as M
     from yalm_amd import runtime
 
-    ndev = int(os.environ.get("YALM_BENCH_NDEV", "0")) or None
+    ndev = 1 if args.rehearse else (int(os.environ.get("YALM_BENCH_NDEV", "0")) or None)
     dev = local_rank if ndev is None else local_rank % ndev
+    cu_part = (local_rank, world) if args.rehearse and world > 1 else None
+    launch = runtime.LAUNCH_EAGER if args.eager else 0
     runtime.check(runtime.lib.yalm_set_device(dev))
     base = M.PRESETS[args.model]
     cfg = base.with_(weight_dtype=M.F16 if args.dtype == "fp16" else M.F8E5M2)
 
-    candidates = transport_candidates(world, args.tp, args.tp_transport, args.replicas)
+    candidates = transport_candidates(world, args.tp, "ipc" if args.rehearse else args.tp_transport, args.replicas)
 
     def all_ok(ok):
+        """Every rank's verdict; a failed agreement (a peer that died or timed out inside
+        another collective: ADVICE r5) counts as not ok, so the fallback chain goes on."""
         if dist is None:
             return ok
         oks = [None] * world
-        dist.all_gather_object(oks, ok)
-        return all(oks)
+        try:
+            dist.all_gather_object(oks, ok)
+        except Exception:
+            return False
+        return all(bool(o) for o in oks)
 
     def timed_decode(dec, tp):
         """Hydrate the prompt, warm up, then time exactly args.steps greedy tokens
@@ -583,7 +598,7 @@ def main():
         dm = dec = None
         err = None
         try:
-            dm, dec = make_decoder(runtime, M, cfg, rank, world, mode, dist)
+            dm, dec = make_decoder(runtime, M, cfg, rank, world, mode, dist, launch, cu_part)
         except Exception as e:
             err = f"{mode} failed on rank {rank}: {str(e)[:200]}"
         ok = all_ok(err is None)
@@ -699,6 +714,12 @@ def main():
     out["kernels_per_token"] = kernels_per_token
     if tp and tp_size > 1:
         out["tp"] = tp_info(mode, exch_us, kernels_per_token, cfg, agree)
+    if cu_part is not None:
+        out["n_gpus"] = 1
+        out["config"]["parallelism"] += "-rehearsal"
+        out["rehearsal"] = (f"{world} rank processes on ONE MI355X, each decoder stream on a disjoint block of "
+                            f"{256 // world} CUs (yalm_stream_create_cu_part): config 5's production launch sequence "
+                            "(no shared-GPU gates), NOT a scaling number -- the ranks share one GPU's HBM")
     if fallback:
         out["fallback"] = fallback
     dec.close()
@@ -718,7 +739,7 @@ def main():
             # others' barriers out of step)
             ok2, err2 = 1, None
             try:
-                dm, dec = make_decoder(runtime, M, cfg, rank, world, "tp-ipc", dist)
+                dm, dec = make_decoder(runtime, M, cfg, rank, world, "tp-ipc", dist, launch, cu_part)
             except Exception as e:
                 ok2, err2 = 0, e
             oks2 = [None] * world

@@ -135,7 +135,10 @@ int yalm_device_tokens(yalm_decoder d, int *out, int cap, int *n_total);
 /* Block::block (model.cpp:213-265) for one layer, eagerly, on the decoder's
  * current activation x (the test hook for per-layer parity). */
 int yalm_block(yalm_decoder d, int layer, int pos, int kv_sink, int kv_pos, int kv_len);
-/* Host access to the decoder's activation x (dim floats) and logits. */
+/* Host access to the decoder's activation x (dim floats) and logits. After a
+ * YALM_HYDRATE_KV_CACHE forward of an IPC tensor-parallel decoder x is undefined
+ * (that forward's last W2 partial is never exchanged: nothing reads it); after
+ * yalm_block and OUTPUT forwards it is the full hidden state on every rank. */
 int yalm_get_x(yalm_decoder d, float *host);
 int yalm_set_x(yalm_decoder d, const float *host);
 int yalm_get_logits(yalm_decoder d, float *host);
@@ -172,10 +175,20 @@ const char *yalm_kernel_name(yalm_decoder d, int kernel_id);
 /* 1 if this decoder's launch path runs attention and the Wo projection (+ the
  * residual add) as ONE launch (attn_wo.h: the Wo weight stream overlaps the
  * attention; replaces attn + fused_matmul_add_residuals, infer.cu:338-524, 270):
- * single GPU, head_dim 128, fp16 / fp8 weights with 4 or 8 KB Wo rows, and
- * YALM_ATTN_WO not 0 at creation. 0 = two separate launches. The split-KV
+ * head_dim 128, fp16 / fp8 weights with 1, 2, 4 or 8 KB (per-rank) Wo rows, and
+ * not YALM_LAUNCH_SEPARATE_ATTN_WO. 0 = two separate launches. The split-KV
  * attention output is handed to the Wo workgroups as {value, epoch} granules. */
 int yalm_decoder_attn_wo(yalm_decoder d);
+/* Launch-mode switches of one decoder (default 0; drops captured graphs):
+ * YALM_LAUNCH_EAGER every forward launches its kernels directly instead of replaying
+ * the per-token graph (profilers that mis-handle graph replay); YALM_LAUNCH_SYNC a
+ * stream sync after every replay (debugging); YALM_LAUNCH_SEPARATE_ATTN_WO separate
+ * attention and Wo launches where the fused one would run (A/B and tests). The
+ * production library reads no environment variable. */
+#define YALM_LAUNCH_EAGER 1
+#define YALM_LAUNCH_SYNC 2
+#define YALM_LAUNCH_SEPARATE_ATTN_WO 4
+int yalm_decoder_set_launch(yalm_decoder d, int flags);
 /* The fused launch's plan for a (per-rank) config when `slots` workgroups of 256
  * threads are co-resident (occupancy x CUs): returns 1 and the key splits per kv head
  * and the grid size, or 0 = separate attention and Wo launches (unsupported shape, or
@@ -214,10 +227,15 @@ int yalm_decoder_create_tp(const yalm_config *config, const yalm_model_weights *
                            const void *unique_id, yalm_stream s, yalm_decoder *out);
 /* The same split with an IPC one-shot exchange instead of RCCL (no NCCL
  * communicator; also runs several ranks on ONE GPU, which RCCL refuses): each
- * rank allocates its exchange buffer (yalm_tp_ipc_alloc, config = full model)
- * and shares the 64-byte hipIpcMemHandle out of band; every rank then passes
- * all tp_size handles (rank order; its own entry is ignored). The decoder
- * takes ownership of own_buf (1..8 ranks). Per exchange no launch of its own:
+ * rank allocates its exchange buffer (yalm_tp_ipc_alloc, config = full model,
+ * s = the stream its decoder will run on) and shares the YALM_TP_HANDLE_BYTES
+ * rank record out of band (the buffer's hipIpcMemHandle, the GPU's UUID and the
+ * stream's CU mask); every rank then passes all tp_size records (rank order)
+ * and the same stream s. Ranks on one GPU whose CU masks overlap get a one-wave
+ * gate launch before each exchange consumer (they could otherwise hold the CUs a
+ * peer's producer needs); one GPU per rank, or disjoint CU masks
+ * (yalm_stream_create_cu_part), run the production sequence without it. The
+ * decoder takes ownership of own_buf (1..8 ranks). Per exchange no launch of its own:
  * the producer (the fused attention + Wo launch, the W2 GEMV, the logits GEMV,
  * the argmax) pushes each value of this rank's partial into this rank's slot of
  * EVERY rank's buffer as an 8-byte {value, tag} granule (one system-scope store:
@@ -226,7 +244,15 @@ int yalm_decoder_create_tp(const yalm_config *config, const yalm_model_weights *
  * in rank order, so x is identical on every rank. Past 4 ranks a collect launch
  * sums x once before the consumer. The exchange sequence numbers live in the
  * decoder's step state, so every rank must make the same calls in lockstep. */
-int yalm_tp_ipc_alloc(const yalm_config *config, int tp_size, void **buf, void *handle_out);
+#define YALM_TP_HANDLE_BYTES 128
+#define YALM_CU_MASK_WORDS 8 /* 256 CUs */
+int yalm_tp_ipc_alloc(const yalm_config *config, int tp_size, yalm_stream s, void **buf, void *handle_out);
+/* A stream restricted to CU block `part` of `n_parts` (CUs [part * ncu / n_parts,
+ * (part + 1) * ncu / n_parts), spread by the driver over all XCDs): n_parts rank
+ * processes on ONE GPU then run on disjoint CUs like n_parts small GPUs (the
+ * one-GPU rehearsal of tensor parallelism; tests/test_gpu_mistral_dims.py, bench.py
+ * --rehearse). Destroy with yalm_stream_destroy. */
+int yalm_stream_create_cu_part(int part, int n_parts, yalm_stream *out);
 int yalm_decoder_create_tp_ipc(const yalm_config *config, const yalm_model_weights *weights, int tp_rank, int tp_size,
                                void *own_buf, const void *handles, yalm_stream s, yalm_decoder *out);
 /* Device-to-device 2D copy (hipMemcpy2D): shard slicing of weights resident in HBM. */
@@ -246,8 +272,26 @@ int yalm_copy_2d(void *dst, size_t dst_pitch, const void *src, size_t src_pitch,
  * dims multiple of 128, head_dim 64 | 128 and pos0 + n <= max_seq_len
  * (the sliding window past max_seq_len stays on the decode path).
  * Synchronous. Activations are rounded to f16 for the MFMA inputs: results
- * match the decode path within the tolerance stated in tests/test_gpu_prefill.py. */
+ * match the decode path within the tolerance stated in tests/test_gpu_prefill.py.
+ * Range guard: where the reference's f32 activations would not fit an f16 operand,
+ * a layer's GLU output (W2's A operand; trained checkpoints' "massive activations")
+ * is stored with an exact power-of-two scale that W2's epilogue undoes, and the pass
+ * runs again; any other operand out of range (the normalised x, Q) returns
+ * YALM_ERR_UNSUPPORTED (the decode path keeps them in f32). */
 int yalm_prefill(yalm_decoder d, const int *tokens, int n, int pos0, float *logprobs);
+/* The last yalm_prefill's passes (1 = no operand out of range) and the number of
+ * layers whose GLU output ran scaled. */
+int yalm_prefill_info(yalm_decoder d, int *passes, int *scaled_layers);
+/* Precision form of decoder d's prefill. YALM_PREFILL_FAST (default): f16 activation
+ * operands (the K / V columns' over a split [hi | lo] operand). YALM_PREFILL_SPLIT: every
+ * activation operand -- the normalised x, Q, the attention probabilities P, the attention
+ * output, the GLU output -- as f16 [hi | lo] pairs (~22 significant bits, the f32 the
+ * reference keeps, to ~2^-22), at twice the matrix work; the perplexity bar of SURVEY §7
+ * (|d log ppl| <= 1e-3) then holds on peaked models too. The CLI's
+ * -m perplexity uses SPLIT, prompt hydration FAST. */
+#define YALM_PREFILL_FAST 0
+#define YALM_PREFILL_SPLIT 1
+int yalm_set_prefill_precision(yalm_decoder d, int mode);
 /* Average device time (ms) of one n-position prefill with log-probs (synthetic
  * token ids), over `iters` back-to-back runs (bench_prefill.py). */
 int yalm_prefill_time(yalm_decoder d, int n, int iters, float *avg_ms);

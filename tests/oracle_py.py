@@ -122,13 +122,14 @@ def ffn(x, w1, w2, w3, act, dtype):
     return out
 
 
-def synth_host_tensors_fast(cfg: M.ModelConfig, seed: int = 1, peak: float = 1.0) -> dict:
+def synth_host_tensors_fast(cfg: M.ModelConfig, seed: int = 1, peak: float = 1.0, real: "M.Realistic" = None) -> dict:
     """Full-size twin of DeviceModel.synthetic() built by the oracle's C
-    initialiser (OpenMP): same hash, same bits."""
+    initialiser (OpenMP): same hash, same bits; real: the realistic model's patches
+    (models.realistic_patch) applied the same way."""
     out = {}
     for name, (shape, is_norm) in M.tensor_shapes(cfg).items():
         n = int(np.prod(shape))
-        scale, offset = M.synth_params(name, is_norm, peak)
+        scale, offset = M.synth_params(name, is_norm, peak, real)
         s = M.synth_seed(seed, name)
         if is_norm:
             a = np.empty(n, np.float32)
@@ -143,7 +144,7 @@ def synth_host_tensors_fast(cfg: M.ModelConfig, seed: int = 1, peak: float = 1.0
             a = np.empty(n, np.uint8)
             olib.orc_synth_f8(P(a), n, s, scale)
         out[name] = a.reshape(shape)
-    return out
+    return M.apply_realistic(cfg, out, real) if real is not None else out
 
 
 class OracleModel:

@@ -49,8 +49,7 @@ def make(cfg, seed, fused=True, t=None, extra=None):
     if t is None:
         t = M.synth_host_tensors(cfg, seed=seed)
     dm = runtime.DeviceModel.from_arrays(cfg, t)
-    env = {"YALM_ATTN_WO": "1" if fused else "0"}
-    env.update(extra or {})
+    env = dict(extra or {})
     old = {k: os.environ.get(k) for k in env}
     for k, v in env.items():
         if v is None:
@@ -58,7 +57,7 @@ def make(cfg, seed, fused=True, t=None, extra=None):
         else:
             os.environ[k] = v
     try:
-        dec = runtime.Decoder(dm)
+        dec = runtime.Decoder(dm, launch=0 if fused else runtime.LAUNCH_SEPARATE_ATTN_WO)
     finally:
         for k, v in old.items():
             if v is None:

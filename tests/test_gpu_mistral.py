@@ -48,8 +48,8 @@ def test_mistral_shape_greedy_parity(dtype):
         dm.close()
 
 
-@pytest.mark.parametrize("peak", [1.0, M.PEAKED], ids=["uniform", "peaked"])
-def test_mistral_config2_256_tokens_vs_oracle(peak):
+@pytest.mark.parametrize("real", [None, M.REALISTIC], ids=["uniform", "realistic"])
+def test_mistral_config2_256_tokens_vs_oracle(real):
     """The config-2 workload as written (BASELINE.json: Mistral-7B fp16, all 32 layers,
     256 greedy tokens after the bench's 13-token prompt, kv_len up to 268) against the
     CPU oracle step by step: logits within 1e-3 rel at every step, the device's argmax
@@ -57,18 +57,21 @@ def test_mistral_config2_256_tokens_vs_oracle(peak):
     (the sequence then continues with the device's token), and the device greedy loop
     (one graph replay per token, argmax on the device) reproduces the sequence.
 
-    peaked: the same model with the final norm weight x M.PEAKED, so the
-    next-token distributions are as peaked as a trained checkpoint's (top-1 probability
-    >= 0.5 at most steps, log ppl of the greedy text << ln(vocab)); the default synthetic
-    model's are near-uniform (logit std ~1.2)."""
+    realistic (round 5's "peaked" model only scaled the final norm by 2^3,
+    an exact logit scale that could not change a token): models.REALISTIC, hidden states with
+    a trained checkpoint's regimes -- peaked attention softmax (Wq / Wk x 12), three residual
+    outlier channels of 10^2..10^3 (embedding columns, W2 rows), a GLU product above 65504 at
+    every position in layer 1, a final norm x 0.7; next-token distributions peaked (top-1
+    probability >= 0.5 at most steps, log ppl of the greedy text << ln(vocab)). The default
+    synthetic model's are near-uniform (logit std ~1.2)."""
     from yalm_amd import runtime
 
     cfg = M.MISTRAL_7B.with_(weight_dtype=M.F16)
-    dm = runtime.DeviceModel.synthetic(cfg, seed=1, peak=peak)
+    dm = runtime.DeviceModel.synthetic(cfg, seed=1, real=real)
     dec = runtime.Decoder(dm)
     dec2 = runtime.Decoder(dm)
     try:
-        om = O.OracleModel(cfg, O.synth_host_tensors_fast(cfg, seed=1, peak=peak))
+        om = O.OracleModel(cfg, O.synth_host_tensors_fast(cfg, seed=1, real=real))
         prompt = [(7 * i + 1) % cfg.vocab_size for i in range(13)]  # bench.py's prompt
         for pos, t in enumerate(prompt[:-1]):
             dec.forward(t, pos, runtime.HYDRATE_KV_CACHE)
@@ -91,11 +94,11 @@ def test_mistral_config2_256_tokens_vs_oracle(peak):
             seq.append(tg)
             tok, pos = tg, pos + 1
         p1 = np.array(p1)
-        print(f"peak {peak}: 256 tokens, kv_len {len(prompt)}..{pos}: worst logits rel {worst:.2e}, near-tie steps "
+        print(f"{'realistic' if real else 'uniform'}: 256 tokens, kv_len {len(prompt)}..{pos}: worst logits rel {worst:.2e}, near-tie steps "
               f"{near_ties}; oracle top-1 probability median {np.median(p1):.3f}, >= 0.5 at {np.mean(p1 >= 0.5):.0%} "
               f"of steps; log ppl of the greedy text {-np.mean(lp):.3f} (ln vocab {np.log(cfg.vocab_size):.2f})")
         assert near_ties <= 4
-        if peak > 1:
+        if real is not None:
             assert np.mean(p1 >= 0.5) >= 0.5 and -np.mean(lp) < 0.25 * np.log(cfg.vocab_size)
         dev = dec2.generate_greedy(prompt[-1], len(prompt) - 1, 256)
         assert list(dev) == seq

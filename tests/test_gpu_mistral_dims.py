@@ -80,11 +80,17 @@ class Pair:
             rt().lib.yalm_free(p)
 
 
-@pytest.fixture(scope="module", params=[M.F16, M.F8E5M2], ids=["f16", "fp8"])
+@pytest.fixture(scope="module", params=[(M.F16, None), (M.F8E5M2, None), (M.F16, M.REALISTIC)],
+                ids=["f16", "fp8", "f16-realistic"])
 def model(request):
-    cfg = CFG.with_(weight_dtype=request.param)
-    host = O.synth_host_tensors_fast(cfg, seed=3)
-    dm = rt().DeviceModel.synthetic(cfg, seed=3)
+    """realistic: models.REALISTIC -- peaked attention, residual outlier
+    channels of 10^2..10^3, a GLU product above 65504 in layer 1 (f32 on both sides in the
+    decode), a final norm scale that is not a power of two."""
+    dtype, real = request.param
+    cfg = CFG.with_(weight_dtype=dtype)
+    host = O.synth_host_tensors_fast(cfg, seed=3, real=real)
+    dm = rt().DeviceModel.synthetic(cfg, seed=3, real=real)
+    dm.real = real
     yield cfg, host, dm
     dm.close()
 
@@ -117,9 +123,9 @@ def test_16k_window_decode_into_sink_regime(model):
     every attention workgroup walks several chunks and the mergers fold many splits. Cache
     rows 0 .. 16377 hydrated, then 16 positions decoded across max_seq_len into the sink
     regime against the oracle, same bars as test_full_window_decode_into_sink_regime."""
-    cfg0, host, _ = model
-    if cfg0.weight_dtype != M.F16:
-        pytest.skip("the window length is independent of the weight type: f16 only")
+    cfg0, host, dm0 = model
+    if cfg0.weight_dtype != M.F16 or dm0.real is not None:
+        pytest.skip("the window length is independent of the weight type and model: f16 uniform only")
     cfg = cfg0.with_(max_seq_len=16384)
     hyd = cfg.max_seq_len - 6
     dm = rt().DeviceModel.synthetic(cfg, seed=3)
@@ -190,11 +196,15 @@ def _tp_worker(rank, size, port, q):
             dist.all_gather_object(out, h)
             return out
 
-        dec = R.Decoder(dm, tp_gather=gather)
+        # each rank decodes on its own block of 256 / size CUs: the ranks run like `size` small
+        # GPUs, so the production launch sequence runs (no shared-GPU gates, fused attention +
+        # Wo on every rank; size 8: the collect form)
+        dec = R.Decoder(dm, tp_gather=gather, cu_part=(rank, size))
+        kernels, fused = dec.graph_kernels(2), dec.attn_wo
         prompt = [1, 415, 3195, 28713, 264, 9]
         logits = [dec.forward(t, pos) for pos, t in enumerate(prompt)]
         toks = dec.generate_greedy(int(np.argmax(logits[-1])), len(prompt), 12)
-        q.put((rank, [lg.copy() for lg in logits], toks))
+        q.put((rank, [lg.copy() for lg in logits], toks, kernels, fused))
         dec.close()
         dm.close()
     finally:
@@ -203,15 +213,17 @@ def _tp_worker(rank, size, port, q):
 
 @pytest.mark.parametrize("size", [2, 4, 8])
 def test_tensor_parallel_ipc_mistral_dims_vs_oracle(size):
-    """TP over `size` processes on this GPU (the launch-lean IPC exchange, tp_exchange.h;
-    RCCL refuses two ranks on one GPU) at Mistral dims: every rank's logits identical,
-    and equal to the CPU oracle's within 1e-3; greedy tokens identical to the oracle.
-    Sizes 2 and 4 sum the exchanged x inside the consuming GEMVs; size 8 runs the
-    collect form (a collect launch before each consumer, TPX_STAGE_MAX_RANKS) and, with
-    8 fused grids unable to share one GPU, the separate attention and Wo launches.
-    size 8 is the TP8 geometry of BASELINE config 5: per rank 1 kv head and 4 q
-    heads (Wq 512 rows, Wk / Wv 128), Wo 512 columns, W1 / W3 1792 rows, W2 1792
-    columns, a 4000-row vocabulary slice (argmax pick over 8 shards)."""
+    """Config 5's production sequence rehearsed on this one GPU: TP over
+    `size` processes, each rank's decoder stream on a disjoint block of 256 / size CUs
+    (yalm_stream_create_cu_part), the launch-lean IPC exchange (tp_exchange.h; RCCL
+    refuses two ranks on one GPU) at Mistral dims. Checked: the fused attention + Wo launch
+    runs on every rank; no shared-GPU gate launches (kernels per token = one GPU's up to 4
+    ranks, + the 2 L collect launches at 8); every rank's logits identical and equal to the
+    CPU oracle's within 1e-3; greedy tokens identical to the oracle. Sizes 2 and 4 sum the
+    exchanged x inside the consuming GEMVs (their in-GEMV cross-rank wait runs for real);
+    size 8 is the TP8 geometry of BASELINE config 5: per rank 1 kv head and 4 q heads (Wq
+    512 rows, Wk / Wv 128), Wo 512 columns, W1 / W3 1792 rows, W2 1792 columns, a 4000-row
+    vocabulary slice (argmax pick over 8 shards), the collect form before each consumer."""
     import queue
     import socket
     import time
@@ -242,6 +254,10 @@ def test_tensor_parallel_ipc_mistral_dims_vs_oracle(size):
         for a, b in zip(res[0][1], r[1]):
             np.testing.assert_array_equal(a, b)
         assert r[2] == res[0][2]
+    one_gpu = 4 * CFG.n_layers + 3  # step_begin, 4 per layer, logits, argmax
+    want_k = one_gpu + (2 * CFG.n_layers if size > 4 else 0)  # the collect form past 4 ranks
+    assert all(r[4] for r in res), "the fused attention + Wo launch must run on every rank"
+    assert all(r[3] == want_k for r in res), ([r[3] for r in res], want_k)
     host = O.synth_host_tensors_fast(CFG, seed=3)
     om = O.OracleModel(CFG, host)
     prompt = [1, 415, 3195, 28713, 264, 9]

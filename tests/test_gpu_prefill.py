@@ -241,3 +241,119 @@ def test_bench_prefill_leg():
     assert rl["bound"] == "mfma" and 0 < rl["achieved"] and 0 < rl["frac"] < 1
     assert out["flops"] > 0 and out["tok_per_s"] > 0
     assert out["spot_check"]["max_abs_dlogp_vs_decode"] <= LP_ATOL
+
+
+def _f16_twin(cfg8, t8):
+    """The f16 model whose weights are the E5M2 model's, upcast exactly (byte b -> f16 bits
+    b << 8): what the fp8 prefill's dequantised copy must compute with."""
+    t16 = {}
+    for name, a in t8.items():
+        t16[name] = a if a.dtype == np.float32 else (a.astype(np.uint16) << 8).view(np.float16)
+    return cfg8.with_(weight_dtype=M.F16), t16
+
+
+@pytest.mark.parametrize("cfg_name", ["gqa-d128", "d768"])
+@pytest.mark.parametrize("n", [13, 200])
+def test_fp8_prefill_equals_f16_twin(cfg_name, n):
+    """an fp8 (E5M2) model through yalm_prefill (per-layer exact upcast of
+    the weights to f16, then the f16 MFMA GEMMs; the short-prompt skinny path at 13) is BIT
+    for bit the prefill of its f16 twin -- log p and the KV cache (the next decode step's
+    logits) -- and matches the fp8 decode engine run position by position within LP_ATOL."""
+    cfg8 = CFGS[cfg_name].with_(weight_dtype=M.F8E5M2)
+    t8 = M.synth_host_tensors(cfg8, seed=11)
+    cfg16, t16 = _f16_twin(cfg8, t8)
+    R = rt()
+    dm8, dm16 = R.DeviceModel.from_arrays(cfg8, t8), R.DeviceModel.from_arrays(cfg16, t16)
+    d8, d16, dd = R.Decoder(dm8), R.Decoder(dm16), R.Decoder(dm8)
+    try:
+        tokens = np.random.default_rng(31 + n).integers(0, cfg8.vocab_size, size=n).astype(np.int32)
+        lp8, lp16 = d8.prefill(tokens), d16.prefill(tokens)
+        np.testing.assert_array_equal(lp8, lp16)
+        np.testing.assert_array_equal(d8.forward(9, n), d16.forward(9, n))  # the KV cache rows, bit for bit
+        assert np.max(np.abs(lp8[: n - 1] - _decode_logprobs(dd, tokens))) <= LP_ATOL
+    finally:
+        for h in (d8, d16, dd, dm8, dm16):
+            h.close()
+
+
+def test_prefill_range_guard_scales_glu_output():
+    """a GLU product above 65504 (the f16 range; the reference keeps it in
+    f32, infer.cpp:360-375) must not become inf. models.REALISTIC's spike layer gives one at
+    every position: the range guard re-runs the pass with that layer's GLU output scaled by an
+    exact power of two (prefill.h range_note), so log p and the next decode step match the
+    decode engine, which keeps the product in f32."""
+    cfg = M.LLAMA_32_3B.with_(n_layers=2, max_seq_len=256)  # the spike needs the real dims' norms
+    R = rt()
+    dm = R.DeviceModel.synthetic(cfg, seed=4, real=M.REALISTIC)
+    dec_p, dec_d = R.Decoder(dm), R.Decoder(dm)
+    try:
+        for n in (17, 150):  # the skinny and the large-tile GEMMs
+            tokens = np.random.default_rng(n).integers(0, cfg.vocab_size, size=n).astype(np.int32)
+            lp = dec_p.prefill(tokens)
+            passes, scaled = dec_p.prefill_info()
+            assert passes == 2 and scaled == 1, (passes, scaled)
+            assert np.all(np.isfinite(lp))
+            ld = _decode_logprobs(dec_d, tokens)
+            assert np.max(np.abs(lp[: n - 1] - ld)) <= LP_ATOL
+            dec_d.forward(int(tokens[-1]), n - 1)
+            lg_p, lg_d = dec_p.forward(7, n), dec_d.forward(7, n)
+            assert np.max(np.abs(lg_p - lg_d)) / np.max(np.abs(lg_d)) < 5e-3
+        # a model that fits: one pass
+        dmu = R.DeviceModel.synthetic(cfg, seed=4)
+        du = R.Decoder(dmu)
+        du.prefill(np.arange(40, dtype=np.int32))
+        assert du.prefill_info() == (1, 0)
+        du.close()
+        dmu.close()
+    finally:
+        dec_p.close()
+        dec_d.close()
+        dm.close()
+
+
+def test_prefill_range_guard_refuses_unscalable_operand():
+    """An operand the guard does not rescale (here the normalised x: an rms_att weight of
+    1e6 puts one column of it past 65504) is refused with YALM_ERR_UNSUPPORTED instead of
+    returning inf / NaN log-probs."""
+    cfg = CFGS["gqa-d128"]
+    t = M.synth_host_tensors(cfg, seed=4)
+    t["model.layers.1.attn.norm.weight"][5] = 1e6
+    R = rt()
+    dm = R.DeviceModel.from_arrays(cfg, t)
+    dec = R.Decoder(dm)
+    try:
+        with pytest.raises(R.YalmError) as ei:
+            dec.prefill(np.arange(30, dtype=np.int32))
+        assert "yalm error 3" in str(ei.value) and "normalised x" in str(ei.value), str(ei.value)
+    finally:
+        dec.close()
+        dm.close()
+
+
+@pytest.mark.parametrize("cfg_name", ["gqa-d128", "d768", "small-d64"])
+@pytest.mark.parametrize("n", [40, 200])
+def test_prefill_split_precision_form(cfg_name, n):
+    """the split-operand form (yalm_set_prefill_precision SPLIT: the
+    normalised x, Q, P, O and H as f16 [hi | lo] pairs, ~22 bits) against the decode engine
+    (f32 activations, pinned to the oracle): an order of magnitude inside the fast form's
+    LP_ATOL, and closer than the fast form on the same prompt; the KV cache it leaves drives
+    the decoder. (T = 40: the short-prompt path switches to the large tiles in this form.)"""
+    cfg = CFGS[cfg_name]
+    R = rt()
+    dm = R.DeviceModel.synthetic(cfg, seed=12)
+    tokens = np.random.default_rng(7 + n).integers(0, cfg.vocab_size, size=n).astype(np.int32)
+    dec_s, dec_f, dec_d = R.Decoder(dm), R.Decoder(dm), R.Decoder(dm)
+    dec_s.set_prefill_precision(R.PREFILL_SPLIT)
+    try:
+        lp_s, lp_f = dec_s.prefill(tokens)[: n - 1], dec_f.prefill(tokens)[: n - 1]
+        ld = _decode_logprobs(dec_d, tokens)
+        es, ef = np.max(np.abs(lp_s - ld)), np.max(np.abs(lp_f - ld))
+        print(f"{cfg_name} T {n}: max |d log p| split {es:.2e}, fast {ef:.2e}")
+        assert es <= LP_ATOL / 10, es
+        assert es < ef, (es, ef)
+        dec_d.forward(int(tokens[-1]), n - 1)
+        lg_s, lg_d = dec_s.forward(5, n), dec_d.forward(5, n)
+        assert np.max(np.abs(lg_s - lg_d)) / np.max(np.abs(lg_d)) < 1e-3
+    finally:
+        for h in (dec_s, dec_f, dec_d, dm):
+            h.close()

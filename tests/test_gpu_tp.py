@@ -195,7 +195,7 @@ def _tok(pos):
     return (pos * 7 + 3) % FUSED.vocab_size
 
 
-def _tp_fused_worker(rank, size, port, q):
+def _tp_fused_worker(rank, size, port, q, cu_mask=False):
     import os
 
     import torch.distributed as dist
@@ -213,7 +213,7 @@ def _tp_fused_worker(rank, size, port, q):
             dist.all_gather_object(out, h)
             return out
 
-        dec = R.Decoder(dm, tp_gather=gather)
+        dec = R.Decoder(dm, tp_gather=gather, cu_part=(rank, size) if cu_mask else None)
         kernels = dec.graph_kernels(2)
         fused = dec.attn_wo
         for pos in range(HYDR):  # HYDRATE graph: the last layer's W2 exchange has no consumer
@@ -232,13 +232,17 @@ def _tp_fused_worker(rank, size, port, q):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("cu_mask", [False, True], ids=["shared-cus", "cu-masked"])
 @pytest.mark.parametrize("size", [2, 4])
-def test_tp_ipc_fused_launch_lean_multi_rank(size):
+def test_tp_ipc_fused_launch_lean_multi_rank(size, cu_mask):
     """IPC tensor parallelism over `size` processes on this GPU with the launch-lean path:
     the fused attention + Wo launch on every rank (Wo rows of 2 / 1 KiB), the Wo and W2
     partials pushed to the exchange and summed inside the next GEMV, the argmax exchange
-    inside the argmax launch (here the ranks share one GPU, so each consumer is preceded by a
-    1-wave gate launch: no exchange kernel sums anything); every rank identical; after 1030 hydrated positions, logits at
+    inside the argmax launch; every rank identical. shared-cus: the ranks share every CU of
+    this GPU, so each consumer is preceded by a 1-wave gate launch (no exchange kernel sums
+    anything); cu-masked: each rank decodes on its own CU block (yalm_stream_create_cu_part),
+    the gate-free production sequence with the consumers' in-GEMV wait on a real peer
+    (ADVICE r5). After 1030 hydrated positions, logits at
     kv 1031 .. 1040 (17 key chunks) and past max_seq_len (ring + sinks) within 1e-4 of the
     single-GPU decoder's, 16 greedy tokens identical to it; yalm_block's x under TP within
     1e-5 of the single decoder's."""
@@ -256,7 +260,7 @@ def test_tp_ipc_fused_launch_lean_multi_rank(size):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_tp_fused_worker, args=(r, size, port, q)) for r in range(size)]
+    procs = [ctx.Process(target=_tp_fused_worker, args=(r, size, port, q, cu_mask)) for r in range(size)]
     for p in procs:
         p.start()
     res, t0 = [], time.time()
@@ -279,9 +283,10 @@ def test_tp_ipc_fused_launch_lean_multi_rank(size):
     ref = R.Decoder(dm)
     try:
         assert all(r[2] for r in res), "the fused attention + Wo launch must run on every rank"
-        # ranks sharing this GPU get a 1-wave gate launch before each of the 2 L consumers
-        # (yalm_hip.hip tpx_consume); one GPU per rank has none (TP1 test above: equal counts)
-        assert res[0][1] == ref.graph_kernels(2) + 2 * FUSED.n_layers, (res[0][1], ref.graph_kernels(2))
+        # ranks sharing this GPU's CUs get a 1-wave gate launch before each of the 2 L consumers
+        # (yalm_hip.hip tpx_consume); one GPU per rank, or disjoint CU masks, has none
+        gates = 0 if cu_mask else 2 * FUSED.n_layers
+        assert all(r[1] == ref.graph_kernels(2) + gates for r in res), ([r[1] for r in res], ref.graph_kernels(2))
         for pos in range(HYDR):
             ref.forward(_tok(pos), pos, R.HYDRATE_KV_CACHE)
         for pos, got in zip(range(HYDR, HYDR + 16), res[0][3]):

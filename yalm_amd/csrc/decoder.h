@@ -50,9 +50,9 @@ int device_cu_count();
 
 // Tuning / tracing knobs are read from the environment only in the A/B build
 // (tools/build_ab_lib.sh compiles with -DYALM_AB): the production library's
-// behaviour depends on none of them. Functional switches (YALM_ATTN_WO=0: separate
-// attention and Wo launches; YALM_EAGER / YALM_GRAPH_SYNC: launch mode) are read once
-// at decoder creation in every build.
+// behaviour depends on none of them. Functional switches (separate attention and Wo
+// launches; eager launches; a sync after every replay) are set per decoder through
+// yalm_decoder_set_launch.
 inline const char *ab_env(const char *name) {
 #ifdef YALM_AB
 	return getenv(name);
@@ -78,6 +78,9 @@ struct PrefillBufs {
 	float *rope = nullptr;                     // [cap][head_dim / 2][2]
 	float *skp = nullptr;                      // split-K partials of the short-prompt GEMMs (prefill_skinny.h)
 	size_t skp_floats = 0;
+	unsigned *range = nullptr;                 // [n_layers + 1][4] f16-operand range guard (prefill.h range_note)
+	uint16_t *wdq = nullptr;                   // fp8 models: one layer's (or the classifier's) weights as f16
+	int last_passes = 0, last_scaled = 0;      // the last yalm_prefill: passes run, layers with a scaled GLU output
 };
 
 // Prefill GEMM forms (prefill.hip): per GEMM kind the large-tile width (-1 = auto,
@@ -90,6 +93,8 @@ struct PfForms {
 	bool no_skinny = false; // T <= 64: split-K skinny GEMMs (prefill_skinny.h) unless set
 	bool qkv1 = true;       // the q and k | v GEMMs as ONE two-depth launch when BN 256 fits both
 	bool skl = true;        // skinny GEMMs: weight rows staged by LDS-DMA (prefill_skinny.h)
+	bool split = false;     // split-operand precision form (yalm_set_prefill_precision): every f16
+							// activation operand as [hi | lo], the large-tile GEMMs at every T
 };
 PfForms pf_forms_default(); // prefill.hip: the production forms (A/B build: YALM_PF_FORMS)
 
@@ -115,13 +120,13 @@ struct yalm_decoder_s {
 	hipGraphExec_t exec[N_GRAPHS] = {};
 	long long host_pos = -1;         // position of the next forward as the host knows it (-1: unknown)
 	GemvCfg gemv[GK_N];
-	bool eager = false;     // YALM_EAGER=1: launch kernels directly (profilers that mis-handle graph replay)
+	bool eager = false;     // YALM_LAUNCH_EAGER: launch kernels directly (profilers that mis-handle graph replay)
 	// the device greedy loop (yalm_enqueue_greedy / yalm_generate_greedy) launches its forwards
 	// directly rather than replaying GRAPH_GREEDY: measured 0.6-1.1% faster on MI355X in six
 	// interleaved rounds (profiles/r5y_graph_vs_eager.txt); the host issues the 131 launches of
 	// a token well inside the token's 1.6-2.5 ms. A/B builds: YALM_GREEDY_GRAPH=1 replays.
 	bool greedy_eager = true;
-	bool graph_sync = false; // YALM_GRAPH_SYNC=1: synchronise after every replay
+	bool graph_sync = false; // YALM_LAUNCH_SYNC: synchronise after every replay
 	std::string kname;
 	PrefillBufs pf;
 	PfForms pf_forms;
@@ -145,9 +150,9 @@ struct yalm_decoder_s {
 	TpX tpx{};                       // the exchange descriptor passed to producers / consumers
 	bool tpx_gate = false;           // ranks share this GPU: a 1-wave wait launch before each consumer
 	bool tpx_collect = false;        // collect form (many ranks): a collect launch sums x before the consumer
-	// launch path: attention + Wo as one launch (attn_wo.h) when supported;
-	// YALM_ATTN_WO=0 selects the two separate kernels
-	bool attn_wo = false;
+	// launch path: attention + Wo as one launch (attn_wo.h) when supported (attn_wo_ok);
+	// YALM_LAUNCH_SEPARATE_ATTN_WO selects the two separate kernels
+	bool attn_wo = false, attn_wo_ok = false;
 	int awo_nb = 0;                  // grid: n_kv * (awo_S + G - 1) attention + n_heads mergers + ceil(dim / AWO_RPW) Wo
 	int awo_S = 0;                   // key-chunk splits per kv head
 	int awo_slots = 0;               // co-resident workgroup slots of the fused launch (occupancy x CUs)

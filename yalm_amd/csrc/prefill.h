@@ -41,6 +41,18 @@ __device__ __forceinline__ uint16_t f2h_bits(float x) {
 	return u;
 }
 
+// Range guard of the f16 MFMA operands: the reference keeps every
+// activation in f32 (infer.cpp:360-375), the prefill rounds them to f16, which is inf past
+// 65504. A lane whose largest |stored value| reaches that (or is NaN) records its largest
+// |unscaled value| in `slot` (float bits; atomicMax orders non-negative floats, NaN above
+// inf). No atomics while everything fits; the host reads the slots after the pass
+// (prefill.hip run_prefill): the GLU output gets an exact power-of-two scale and the pass
+// runs again, any other operand out of range is YALM_ERR_UNSUPPORTED.
+__device__ __forceinline__ void range_note(unsigned *slot, float stored_absmax, float raw_absmax) {
+	if (slot && !(stored_absmax < 65504.0f))
+		atomicMax(slot, __float_as_uint(raw_absmax));
+}
+
 // C/D map of v_mfma_f32_32x32x16: column = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5).
 __device__ __forceinline__ int crow(int reg, int lane) { return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); }
 
@@ -113,7 +125,13 @@ typedef short short4_t __attribute__((ext_vector_type(4)));
 // 16 s + 8 (e >> 2) + 4 h + (e & 3) of the 32-key block) with V^T fragments
 // from hardware-transposed LDS reads. O^T keeps the query on the lane too, so
 // the online-softmax rescale is one per-lane factor.
-template <int D, int KT = AKT>
+//
+// SPLIT (the split-operand precision form, yalm_set_prefill_precision): Q rows are [hi | lo]
+// (2 q_dim wide), S^T = K hi^T + K lo^T; P^T is split too (P = hi + lo, both f16) so
+// O^T += V^T hi^T + V^T lo^T; O is stored as [hi | lo] rows (2 q_dim wide) for the Wo
+// GEMM's split A operand: the f16 roundings of q, P and o are gone, the
+// matrix work doubles.
+template <int D, int KT = AKT, bool SPLIT = false>
 __global__ __launch_bounds__(THREADS) void attn_prefill_kernel(const uint16_t *__restrict__ Q,
                                                                const uint16_t *__restrict__ kc,
                                                                const uint16_t *__restrict__ vc, int T, int pos0,
@@ -139,12 +157,17 @@ __global__ __launch_bounds__(THREADS) void attn_prefill_kernel(const uint16_t *_
 	const float sl2 = 1.4426950408889634f / sqrtf((float)D);
 	const int kv_rows = pos0 + T; // valid cache rows (masked keys past a query are never used)
 
+	constexpr int QS = SPLIT ? 2 : 1; // Q / O row width in q_dim units
 	half8_t qf[D / 16]; // B operand of S^T = K Q^T: Q[query = l32][d = 16 s + 8 h ..]
+	half8_t ql[SPLIT ? D / 16 : 1]; // SPLIT: the lo half of Q
 	{
-		const uint16_t *qp = Q + (size_t)min(qrow, T - 1) * q_dim + h * D + 8 * hh;
+		const uint16_t *qp = Q + (size_t)min(qrow, T - 1) * q_dim * QS + h * D + 8 * hh;
 #pragma unroll
-		for (int s = 0; s < D / 16; ++s)
+		for (int s = 0; s < D / 16; ++s) {
 			qf[s] = *(const half8_t *)(qp + 16 * s);
+			if constexpr (SPLIT)
+				ql[s] = *(const half8_t *)(qp + q_dim + 16 * s);
+		}
 	}
 	f32x16_t o[D / 32]; // O^T tiles: rows = d (32 jd + crow), column = query
 #pragma unroll
@@ -177,6 +200,7 @@ __global__ __launch_bounds__(THREADS) void attn_prefill_kernel(const uint16_t *_
 		// ---- S^T = K Q^T: two 32-key blocks; register r of block j is key key0 + 32 j + crow(r, lane)
 		f32x16_t st[NJ];
 		half8_t pb[NJ][2]; // P^T fragments: [block j][k-step s]
+		half8_t pl[SPLIT ? NJ : 1][2]; // SPLIT: P - f16(P)
 		if (live) {
 #pragma unroll
 			for (int j = 0; j < NJ; ++j) {
@@ -187,6 +211,8 @@ __global__ __launch_bounds__(THREADS) void attn_prefill_kernel(const uint16_t *_
 					const int kcnk = 2 * s + hh;
 					const half8_t ka = *(const half8_t *)(Ks + kr * D + 8 * (kcnk ^ (kr % DCH)));
 					st[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ka, qf[s], st[j], 0, 0, 0);
+					if constexpr (SPLIT)
+						st[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ka, ql[s], st[j], 0, 0, 0);
 				}
 			}
 			// ---- online softmax for this lane's query. Raw scores; the 1/sqrt(D) log2(e)
@@ -228,6 +254,8 @@ __global__ __launch_bounds__(THREADS) void attn_prefill_kernel(const uint16_t *_
 					const float p = __builtin_amdgcn_exp2f(fmaf(st[j][r], sl2, -m));
 					ls += p;
 					pb[j][r >> 3][r & 7] = (_Float16)p;
+					if constexpr (SPLIT)
+						pl[j][r >> 3][r & 7] = (_Float16)(p - (float)pb[j][r >> 3][r & 7]);
 				}
 			ls += xor32(ls);
 			l += ls;
@@ -253,6 +281,8 @@ __global__ __launch_bounds__(THREADS) void attn_prefill_kernel(const uint16_t *_
 							va[4 + e] = __builtin_bit_cast(_Float16, (short)hi[e]);
 						}
 						o[jd] = __builtin_amdgcn_mfma_f32_32x32x16_f16(va, pb[j][s], o[jd], 0, 0, 0);
+						if constexpr (SPLIT)
+							o[jd] = __builtin_amdgcn_mfma_f32_32x32x16_f16(va, pl[j][s], o[jd], 0, 0, 0);
 					}
 				}
 		}
@@ -263,15 +293,28 @@ __global__ __launch_bounds__(THREADS) void attn_prefill_kernel(const uint16_t *_
 	// ---- normalise and store O[query][h * D + d] (f16, the Wo GEMM's A operand); d = 32 jd + crow(r)
 	if (qrow < T) {
 		const float inv = 1.0f / l;
-		uint16_t *op = O + (size_t)qrow * q_dim + h * D;
+		uint16_t *op = O + (size_t)qrow * q_dim * QS + h * D;
 #pragma unroll
 		for (int jd = 0; jd < D / 32; ++jd)
 #pragma unroll
 			for (int r4 = 0; r4 < 4; ++r4) { // registers 4 r4 .. 4 r4 + 3 are 4 consecutive d
 				const int d = 32 * jd + 8 * r4 + 4 * hh;
-				uint32_t w0 = (uint32_t)f2h_bits(o[jd][4 * r4 + 0] * inv) | ((uint32_t)f2h_bits(o[jd][4 * r4 + 1] * inv) << 16);
-				uint32_t w1 = (uint32_t)f2h_bits(o[jd][4 * r4 + 2] * inv) | ((uint32_t)f2h_bits(o[jd][4 * r4 + 3] * inv) << 16);
-				*(uint2 *)(op + d) = make_uint2(w0, w1);
+				float v[4];
+				uint16_t hb[4];
+#pragma unroll
+				for (int e = 0; e < 4; ++e) {
+					v[e] = o[jd][4 * r4 + e] * inv;
+					hb[e] = f2h_bits(v[e]);
+				}
+				*(uint2 *)(op + d) = make_uint2(hb[0] | ((uint32_t)hb[1] << 16), hb[2] | ((uint32_t)hb[3] << 16));
+				if constexpr (SPLIT) {
+					uint16_t lb[4];
+#pragma unroll
+					for (int e = 0; e < 4; ++e)
+						lb[e] = f2h_bits(v[e] - h2f(hb[e]));
+					*(uint2 *)(op + q_dim + d) =
+						make_uint2(lb[0] | ((uint32_t)lb[1] << 16), lb[2] | ((uint32_t)lb[3] << 16));
+				}
 			}
 	}
 }
@@ -292,13 +335,52 @@ __global__ __launch_bounds__(256) void embed_rows_kernel(const int *__restrict__
 	}
 }
 
+// E5M2 weights -> f16 for the prefill of an fp8 model: the byte b is the f16 with bits
+// b << 8 (the decode path's exact upcast), so the f16 MFMA GEMMs over the
+// dequantised copy compute exactly what they compute for the f16 twin model. Up to 8
+// tensors per launch (one launch per layer); 16 bytes in, 32 out per thread step.
+struct DqSegs {
+	const uint8_t *src[8];
+	uint16_t *dst[8];
+	size_t end[8]; // cumulative 16-byte pieces
+	int n;
+};
+__global__ __launch_bounds__(256) void e5m2_to_f16_kernel(DqSegs s) {
+	const size_t total = s.end[s.n - 1];
+	for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+		const uint8_t *sp = s.src[0];
+		uint16_t *dp = s.dst[0];
+		size_t base = 0;
+#pragma unroll
+		for (int m = 1; m < 8; ++m) // constant indices: the kernel-argument arrays stay in SGPRs
+			if (m < s.n && i >= s.end[m - 1]) {
+				sp = s.src[m];
+				dp = s.dst[m];
+				base = s.end[m - 1];
+			}
+		const size_t j = i - base;
+		const u32x4_t v = load_nt16(sp + 16 * j);
+		u32x4_t o[2];
+#pragma unroll
+		for (int q = 0; q < 4; ++q) {
+			const uint32_t w = v[q];
+			o[q >> 1][2 * (q & 1) + 0] = ((w & 0xffu) << 8) | ((w & 0xff00u) << 16);
+			o[q >> 1][2 * (q & 1) + 1] = ((w & 0xff0000u) >> 8) | (w & 0xff000000u);
+		}
+		u32x4_t *d = (u32x4_t *)(dp + 16 * j);
+		d[0] = o[0];
+		d[1] = o[1];
+	}
+}
+
 // Xn[t] = f16(rmsnorm(X[t]) * w)  (rmsnorm, infer.cpp:134-144 statement order).
 // SPLIT: row t of Xn is [hi | lo], 2 dim wide: hi = f16(v), lo = f16(v - hi), so
 // hi + lo carries v to ~22 bits (the K / V columns of the QKV GEMM run over both
 // halves against the same weight row; prefill_gemm.h BWrap).
 template <bool SPLIT>
 __global__ __launch_bounds__(256) void rmsnorm_rows_kernel(const float *__restrict__ X, const float *__restrict__ w,
-                                                           int dim, float eps, uint16_t *__restrict__ Xn) {
+                                                           int dim, float eps, uint16_t *__restrict__ Xn,
+                                                           unsigned *range = nullptr) {
 	__shared__ float red[4];
 	const int t = blockIdx.x;
 	const float *x = X + (size_t)t * dim;
@@ -314,6 +396,7 @@ __global__ __launch_bounds__(256) void rmsnorm_rows_kernel(const float *__restri
 	const float tot = red[0] + red[1] + red[2] + red[3];
 	const float scale = 1.0f / sqrtf(tot / dim + eps);
 	uint16_t *row = Xn + (size_t)t * dim * (SPLIT ? 2 : 1);
+	float ymax = 0.0f;
 	for (int i = threadIdx.x * 4; i < dim; i += 256 * 4) {
 		const float4_t v = *(const float4_t *)(x + i);
 		const float4_t g = *(const float4_t *)(w + i);
@@ -323,6 +406,7 @@ __global__ __launch_bounds__(256) void rmsnorm_rows_kernel(const float *__restri
 		for (int e = 0; e < 4; ++e) {
 			y[e] = v[e] * scale * g[e];
 			hb[e] = f2h_bits(y[e]);
+			ymax = fmaxf(ymax, y[e] != y[e] ? __builtin_inff() : fabsf(y[e])); // NaN counts as inf
 		}
 		*(uint2 *)(row + i) = make_uint2(hb[0] | ((uint32_t)hb[1] << 16), hb[2] | ((uint32_t)hb[3] << 16));
 		if constexpr (SPLIT) {
@@ -334,6 +418,7 @@ __global__ __launch_bounds__(256) void rmsnorm_rows_kernel(const float *__restri
 			    make_uint2(lb[0] | ((uint32_t)lb[1] << 16), lb[2] | ((uint32_t)lb[3] << 16));
 		}
 	}
+	range_note(range, ymax, ymax);
 }
 
 // RoPE (cos, sin) per prompt row and frequency, the decode path's exact

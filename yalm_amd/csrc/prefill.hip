@@ -59,6 +59,8 @@ static int parse_pf_forms(const char *spec, PfForms &f) {
 			f.qkv1 = val != 0, known = true;
 		else if (!strcmp(key, "skl"))
 			f.skl = val != 0, known = true;
+		else if (!strcmp(key, "split"))
+			f.split = val != 0, known = true;
 		if (!known) {
 			set_err(std::string("yalm_set_prefill_forms: unknown key '") + key + "'");
 			return YALM_ERR_ARG;
@@ -79,6 +81,12 @@ PfForms pf_forms_default() {
 
 static PfForms g_test_forms; // the forms of the yalm_gemm_f16 test hook
 
+extern "C" int yalm_set_prefill_precision(yalm_decoder d, int mode) {
+	ARGCHK(d && (mode == YALM_PREFILL_FAST || mode == YALM_PREFILL_SPLIT), "yalm_set_prefill_precision: bad argument");
+	d->pf_forms.split = mode == YALM_PREFILL_SPLIT;
+	return YALM_OK;
+}
+
 extern "C" int yalm_set_prefill_forms(yalm_decoder d, const char *spec) {
 	PfForms f;
 	TRY(parse_pf_forms(spec, f));
@@ -92,6 +100,9 @@ extern "C" int yalm_set_prefill_forms(yalm_decoder d, const char *spec) {
 namespace {
 
 enum { PG_QKV = 0, PG_WO = 1, PG_GLU = 2, PG_W2 = 3, PG_CLS = 4, PG_TEST = 5 };
+// range-guard slots per layer (PrefillBufs::range), in the order the pass produces them;
+// the final norm's operand is slot RG_XATT of row n_layers
+enum { RG_XATT = 0, RG_Q = 1, RG_XFFN = 2, RG_H = 3, RG_N = 4 };
 
 int pf_alloc(yalm_decoder_s *d, void **p, size_t bytes) {
 	HIPCHK(hipMalloc(p, bytes ? bytes : 4));
@@ -280,35 +291,61 @@ pf::BSrc one(const void *w, int rows) {
 	return b;
 }
 
-int launch_attn_prefill(const uint16_t *Q, const uint16_t *kc, const uint16_t *vc, int T, int pos0, int n_heads,
-                        int n_kv, int head_dim, uint16_t *O, hipStream_t st) {
-	const dim3 grid(n_heads, (T + pf::AQ - 1) / pf::AQ); // heads fastest: longest-first dispatch
-	static bool attr_set = false;
-	if (!attr_set) {
-		HIPCHK(hipFuncSetAttribute((const void *)pf::attn_prefill_kernel<128>,
-		                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)pf::attn_prefill_lds<128>()));
-		HIPCHK(hipFuncSetAttribute((const void *)pf::attn_prefill_kernel<64>,
-		                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)pf::attn_prefill_lds<64>()));
-		attr_set = true;
+// fp8 models: the tensors (E5M2 bytes, n elements each) dequantised to f16 into b.wdq, end
+// to end; returns their f16 copies in `out` (prefill.h e5m2_to_f16_kernel)
+int dequant(yalm_decoder_s *d, std::initializer_list<std::pair<const void *, size_t>> t, const uint16_t **out,
+			hipStream_t st) {
+	pf::DqSegs s{};
+	size_t off = 0, pieces = 0;
+	for (auto &p : t) {
+		s.src[s.n] = (const uint8_t *)p.first;
+		s.dst[s.n] = d->pf.wdq + off;
+		out[s.n] = s.dst[s.n];
+		pieces += p.second / 16;
+		s.end[s.n] = pieces;
+		off += p.second;
+		++s.n;
 	}
-	if (head_dim == 128)
-		pf::attn_prefill_kernel<128><<<grid, pf::THREADS, pf::attn_prefill_lds<128>(), st>>>(Q, kc, vc, T, pos0,
-		                                                                                       n_heads, n_kv, O);
-	else if (head_dim == 64)
-		pf::attn_prefill_kernel<64><<<grid, pf::THREADS, pf::attn_prefill_lds<64>(), st>>>(Q, kc, vc, T, pos0,
-		                                                                                     n_heads, n_kv, O);
-	else {
-		set_err("prefill attention: head_dim must be 64 or 128");
-		return YALM_ERR_UNSUPPORTED;
-	}
+	const int grid = (int)std::min<size_t>((pieces + 255) / 256, (size_t)device_cu_count() * 8);
+	pf::e5m2_to_f16_kernel<<<grid, 256, 0, st>>>(s);
 	HIPCHK(hipGetLastError());
 	return YALM_OK;
 }
 
+template <int D, bool SPLIT>
+int launch_attn_prefill_t(const uint16_t *Q, const uint16_t *kc, const uint16_t *vc, int T, int pos0, int n_heads,
+						  int n_kv, uint16_t *O, hipStream_t st) {
+	const dim3 grid(n_heads, (T + pf::AQ - 1) / pf::AQ); // heads fastest: longest-first dispatch
+	auto kern = pf::attn_prefill_kernel<D, pf::AKT, SPLIT>;
+	static bool attr_set = false;
+	if (!attr_set) {
+		HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+								   (int)pf::attn_prefill_lds<D>()));
+		attr_set = true;
+	}
+	hipLaunchKernelGGL(kern, grid, dim3(pf::THREADS), pf::attn_prefill_lds<D>(), st, Q, kc, vc, T, pos0, n_heads, n_kv,
+					   O);
+	HIPCHK(hipGetLastError());
+	return YALM_OK;
+}
+
+// split: Q and O rows [hi | lo] (the split-operand form)
+int launch_attn_prefill(const uint16_t *Q, const uint16_t *kc, const uint16_t *vc, int T, int pos0, int n_heads,
+						int n_kv, int head_dim, uint16_t *O, hipStream_t st, bool split = false) {
+	if (head_dim == 128)
+		return split ? launch_attn_prefill_t<128, true>(Q, kc, vc, T, pos0, n_heads, n_kv, O, st)
+					 : launch_attn_prefill_t<128, false>(Q, kc, vc, T, pos0, n_heads, n_kv, O, st);
+	if (head_dim == 64)
+		return split ? launch_attn_prefill_t<64, true>(Q, kc, vc, T, pos0, n_heads, n_kv, O, st)
+					 : launch_attn_prefill_t<64, false>(Q, kc, vc, T, pos0, n_heads, n_kv, O, st);
+	set_err("prefill attention: head_dim must be 64 or 128");
+	return YALM_ERR_UNSUPPORTED;
+}
+
 int check_prefill_shape(const yalm_config &c) {
 	const int q_dim = c.n_heads * c.head_dim, kv_dim = c.n_kv_heads * c.head_dim;
-	if (c.weight_dtype != YALM_F16) {
-		set_err("yalm_prefill: f16 weights only (MFMA f16 operands)");
+	if (c.weight_dtype != YALM_F16 && c.weight_dtype != YALM_F8E5M2) {
+		set_err("yalm_prefill: f16 or fp8 (E5M2) weights only (MFMA f16 operands)");
 		return YALM_ERR_UNSUPPORTED;
 	}
 	if (c.dim % pf::BN || c.hidden_dim % pf::BN || q_dim % pf::BN || kv_dim % pf::BN || c.vocab_size % pf::BN ||
@@ -328,9 +365,10 @@ int ensure_bufs(yalm_decoder_s *d) {
 	const size_t ntiles = (size_t)c.vocab_size / pf::BN;
 	TRY(pf_alloc(d, (void **)&b.X, cap * c.dim * 4));
 	TRY(pf_alloc(d, (void **)&b.Xn, cap * c.dim * 2 * 2));
-	TRY(pf_alloc(d, (void **)&b.Q, cap * q_dim * 2));
-	TRY(pf_alloc(d, (void **)&b.O, cap * q_dim * 2));
-	TRY(pf_alloc(d, (void **)&b.H, cap * c.hidden_dim * 2));
+	// Q, O, H: [hi | lo] rows in the split-operand form, 2x wide
+	TRY(pf_alloc(d, (void **)&b.Q, cap * q_dim * 2 * 2));
+	TRY(pf_alloc(d, (void **)&b.O, cap * q_dim * 2 * 2));
+	TRY(pf_alloc(d, (void **)&b.H, cap * c.hidden_dim * 2 * 2));
 	TRY(pf_alloc(d, (void **)&b.tok, cap * 4));
 	TRY(pf_alloc(d, (void **)&b.tgt, cap * 4));
 	TRY(pf_alloc(d, (void **)&b.pmax, cap * ntiles * 4));
@@ -338,6 +376,12 @@ int ensure_bufs(yalm_decoder_s *d) {
 	TRY(pf_alloc(d, (void **)&b.tgt_logit, cap * 4));
 	TRY(pf_alloc(d, (void **)&b.lp, cap * 4));
 	TRY(pf_alloc(d, (void **)&b.rope, cap * c.head_dim * 4));
+	TRY(pf_alloc(d, (void **)&b.range, (size_t)(c.n_layers + 1) * RG_N * 4));
+	if (c.weight_dtype == YALM_F8E5M2) { // the f16 copy of one layer's weights, or of the classifier
+		const size_t layer = ((size_t)q_dim + 2 * (size_t)c.n_kv_heads * c.head_dim) * c.dim + (size_t)c.dim * q_dim +
+							 3 * (size_t)c.dim * c.hidden_dim;
+		TRY(pf_alloc(d, (void **)&b.wdq, 2 * std::max(layer, (size_t)c.vocab_size * c.dim)));
+	}
 	{ // short-prompt split-K partials: the largest [KS][64][Np] of the layer's GEMMs
 		const int kv_dim = c.n_kv_heads * c.head_dim, TP = SK_MAX_T;
 		const int np_qkv = (int)q_dim + 2 * kv_dim;
@@ -355,33 +399,43 @@ int ensure_bufs(yalm_decoder_s *d) {
 }
 
 template <int ACT>
-int enqueue_glu(yalm_decoder_s *d, const yalm_block_weights &w, int T) {
+int enqueue_glu(yalm_decoder_s *d, const yalm_block_weights &w, int T, float hscale, unsigned *range) {
 	const yalm_config &c = d->c;
 	const PfForms &f = d->pf_forms;
 	const int bn = pick_bn(f, PG_GLU, T, 2 * c.hidden_dim, true);
+	const int sp = f.split ? 2 : 1; // split-operand form: A = [hi | lo] (K = 2 dim), H rows [hi | lo]
 	pf::E16Glu<ACT> e;
 	e.h = d->pf.H;
-	e.ldh = c.hidden_dim;
+	e.ldh = c.hidden_dim * sp;
 	e.M = T;
+	e.hscale = hscale;
+	e.range = range;
+	e.lo_off = f.split ? c.hidden_dim : 0;
 	pf::BRowsGlu<64> bm{(const uint16_t *)w.w1, (const uint16_t *)w.w3};
 	if (bn == 256)
-		return launch_g16_t<pf::E16Glu<ACT>, pf::BRowsGlu<64>, 256, 2>(f, d->pf.Xn, c.dim, T, c.dim, c.dim, bm,
-		                                                             2 * c.hidden_dim, e, d->stream);
+		return launch_g16_t<pf::E16Glu<ACT>, pf::BRowsGlu<64>, 256, 2>(f, d->pf.Xn, sp * c.dim, T, sp * c.dim, c.dim,
+                                                                     bm, 2 * c.hidden_dim, e, d->stream);
 	if (bn == 128)
-		return launch_g16_t<pf::E16Glu<ACT>, pf::BRowsGlu<64>, 128, 4>(f, d->pf.Xn, c.dim, T, c.dim, c.dim, bm,
-		                                                             2 * c.hidden_dim, e, d->stream);
+		return launch_g16_t<pf::E16Glu<ACT>, pf::BRowsGlu<64>, 128, 4>(f, d->pf.Xn, sp * c.dim, T, sp * c.dim, c.dim,
+                                                                     bm, 2 * c.hidden_dim, e, d->stream);
 	set_err("prefill GLU GEMM: 2 x hidden_dim must divide by 128 (or by a forced width of 128 / 256)");
 	return YALM_ERR_UNSUPPORTED;
 }
 
-// The whole prefill on d->stream: T rows at positions pos0 .. pos0 + T - 1.
-int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
+// The whole prefill on d->stream: T rows at positions pos0 .. pos0 + T - 1. hexp[l] (null:
+// all 0): layer l's GLU output is stored as f16(h * 2^-hexp[l]) and W2 adds 2^hexp[l] x its
+// product (exact power-of-two scales; yalm_prefill chooses them from the range guard).
+int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp, const int *hexp = nullptr) {
 	const yalm_config &c = d->c;
 	const PfForms &f = d->pf_forms;
 	PrefillBufs &b = d->pf;
 	hipStream_t st = d->stream;
 	const int q_dim = c.n_heads * c.head_dim, kv_dim = c.n_kv_heads * c.head_dim;
-	pf::embed_rows_kernel<WF16><<<T, 256, 0, st>>>(b.tok, d->emb, c.dim, b.X);
+	const bool fp8 = c.weight_dtype == YALM_F8E5M2;
+	if (fp8)
+		pf::embed_rows_kernel<WF8><<<T, 256, 0, st>>>(b.tok, d->emb, c.dim, b.X);
+	else
+		pf::embed_rows_kernel<WF16><<<T, 256, 0, st>>>(b.tok, d->emb, c.dim, b.X);
 	HIPCHK(hipGetLastError());
 	const int half = c.head_dim / 2;
 	pf::rope_table_kernel<<<(T * half + 255) / 256, 256, 0, st>>>(d->inv_freq, half, T, pos0, b.rope);
@@ -401,12 +455,27 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 	const int ks_wo = sk_pick_ks({{c.dim, q_dim, 1}}, TP);
 	const int ks_glu = sk_pick_ks({{2 * c.hidden_dim, c.dim, 1}}, TP);
 	const int ks_w2 = sk_pick_ks({{c.dim, c.hidden_dim, 1}}, TP);
-	const bool small = T <= SK_MAX_T && !f.no_skinny && ks_qkv > 0 && ks_wo > 0 && ks_glu > 0 && ks_w2 > 0;
+	const bool small = T <= SK_MAX_T && !f.no_skinny && !f.split && ks_qkv > 0 && ks_wo > 0 && ks_glu > 0 && ks_w2 > 0;
+	// the split-operand precision form (yalm_set_prefill_precision): every activation operand
+	// [hi | lo] -- the normalised x of all three norms, Q, P (attention.h SPLIT), O and H --
+	// each GEMM over K = 2 x its depth with the B rows wrapping (prefill_gemm.h), so no operand
+	// carries an f16 rounding the reference's f32 lacks; sp = operand width factor
+	const bool split = f.split;
+	const int sp = split ? 2 : 1;
+	const int bn_qkv_all = pick_bn(f, PG_QKV, T, q_dim + 2 * kv_dim, false);
 	for (int l = 0; l < c.n_layers; ++l) {
-		const yalm_block_weights &w = d->b[l];
+		yalm_block_weights w = d->b[l];
+		if (fp8) { // this layer's weights as f16 (exact), in the scratch the previous layer's GEMMs are done with
+			const uint16_t *p[7];
+			const size_t qd = (size_t)q_dim * c.dim, kd = (size_t)kv_dim * c.dim, hd = (size_t)c.hidden_dim * c.dim;
+			TRY(dequant(d, {{w.wq, qd}, {w.wk, kd}, {w.wv, kd}, {w.wo, qd}, {w.w1, hd}, {w.w2, hd}, {w.w3, hd}}, p, st));
+			w.wq = p[0], w.wk = p[1], w.wv = p[2], w.wo = p[3], w.w1 = p[4], w.w2 = p[5], w.w3 = p[6];
+		}
 		// normalised x as [hi | lo] (2 dim per row): hi is the q columns' A operand, hi + lo
 		// the k | v columns' (their cache rows then carry one f16 rounding, infer.cpp:299)
-		pf::rmsnorm_rows_kernel<true><<<T, 256, 0, st>>>(b.X, w.rms_att, c.dim, c.norm_eps, b.Xn);
+		unsigned *rg = b.range + (size_t)l * RG_N;
+		const int he = hexp ? hexp[l] : 0;
+		pf::rmsnorm_rows_kernel<true><<<T, 256, 0, st>>>(b.X, w.rms_att, c.dim, c.norm_eps, b.Xn, rg + RG_XATT);
 		HIPCHK(hipGetLastError());
 		{
 			pf::BSrc qkv{};
@@ -427,6 +496,8 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 			e.head_dim = c.head_dim;
 			e.pos0 = pos0;
 			e.clip = c.qkv_clip;
+				e.range = rg + RG_Q;
+				e.q_lo = split ? q_dim : 0;
 			// QKV + clip + RoPE as two GEMMs: q (K = dim over hi) and k | v from column
 			// q_dim (K = 2 dim over hi | lo, the B rows wrapping at dim)
 			if (small) {
@@ -437,7 +508,9 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 				                  st));
 				TRY(launch_skinny_reduce<false>(b.skp, ks_qkv, 2 * ks_qkv, q_dim, T, np, e, st));
 			} else {
-				if (qkv1) { // one launch: the k | v tiles (K = 2 dim) first, then the q tiles (K = dim)
+				if (split) { // q | k | v all over [hi | lo]
+					TRY(launch_plain(f, bn_qkv_all, b.Xn, 2 * c.dim, T, 2 * c.dim, c.dim, qkv, q_dim + 2 * kv_dim, e, st));
+				} else if (qkv1) { // one launch: the k | v tiles (K = 2 dim) first, then the q tiles (K = dim)
 					TRY((launch_g8p<pf::E16QKV, pf::BRowsPlain, 2, 2>(f, b.Xn, 2 * c.dim, T, c.dim, c.dim,
 					                                                   pf::BRowsPlain{qkv}, q_dim + 2 * kv_dim, e, st,
 					                                                   0, q_dim, 2 * c.dim)));
@@ -448,7 +521,7 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 			}
 		}
 		TRY(launch_attn_prefill(b.Q, w.key_cache, w.value_cache, T, pos0, c.n_heads, c.n_kv_heads, c.head_dim, b.O,
-		                        st));
+								st, split));
 		{
 			pf::E16Residual e;
 			e.x = b.X;
@@ -459,45 +532,56 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 				                  b.skp, st));
 				TRY(launch_skinny_reduce<false>(b.skp, ks_wo, ks_wo, c.dim, T, c.dim, e, st));
 			} else {
-				TRY(launch_plain(f, bn_wo, b.O, q_dim, T, q_dim, q_dim, one(w.wo, c.dim), c.dim, e, st));
+				TRY(launch_plain(f, bn_wo, b.O, sp * q_dim, T, sp * q_dim, q_dim, one(w.wo, c.dim), c.dim, e, st));
 			}
 		}
-		pf::rmsnorm_rows_kernel<false><<<T, 256, 0, st>>>(b.X, w.rms_ffn, c.dim, c.norm_eps, b.Xn);
+		if (split)
+			pf::rmsnorm_rows_kernel<true><<<T, 256, 0, st>>>(b.X, w.rms_ffn, c.dim, c.norm_eps, b.Xn, rg + RG_XFFN);
+		else
+			pf::rmsnorm_rows_kernel<false><<<T, 256, 0, st>>>(b.X, w.rms_ffn, c.dim, c.norm_eps, b.Xn, rg + RG_XFFN);
 		HIPCHK(hipGetLastError());
+		const float hscale = ldexpf(1.0f, -he);
 		if (small) {
 			const pf::BRowsGlu<64> bm{(const uint16_t *)w.w1, (const uint16_t *)w.w3};
 			TRY(launch_skinny(f, b.Xn, c.dim, T, c.dim, c.dim, bm, 2 * c.hidden_dim, ks_glu, 0, 2 * c.hidden_dim, b.skp,
 			                  st));
 			if (c.act == YALM_SILU) {
 				pf::E16Glu<1> e;
-				e.h = b.H, e.ldh = c.hidden_dim, e.M = T;
+				e.h = b.H, e.ldh = c.hidden_dim, e.M = T, e.hscale = hscale, e.range = rg + RG_H;
 				TRY(launch_skinny_reduce<true>(b.skp, ks_glu, ks_glu, 2 * c.hidden_dim, T, 2 * c.hidden_dim, e, st));
 			} else {
 				pf::E16Glu<0> e;
-				e.h = b.H, e.ldh = c.hidden_dim, e.M = T;
+				e.h = b.H, e.ldh = c.hidden_dim, e.M = T, e.hscale = hscale, e.range = rg + RG_H;
 				TRY(launch_skinny_reduce<true>(b.skp, ks_glu, ks_glu, 2 * c.hidden_dim, T, 2 * c.hidden_dim, e, st));
 			}
 		} else {
-			TRY(c.act == YALM_SILU ? enqueue_glu<1>(d, w, T) : enqueue_glu<0>(d, w, T));
+			TRY(c.act == YALM_SILU ? enqueue_glu<1>(d, w, T, hscale, rg + RG_H)
+								   : enqueue_glu<0>(d, w, T, hscale, rg + RG_H));
 		}
 		{
 			pf::E16Residual e;
 			e.x = b.X;
 			e.ldx = c.dim;
 			e.M = T;
+			e.scale = ldexpf(1.0f, he);
 			if (small) {
 				TRY(launch_skinny(f, b.H, c.hidden_dim, T, c.hidden_dim, c.hidden_dim, pf::BRowsPlain{one(w.w2, c.dim)},
 				                  c.dim, ks_w2, 0, c.dim, b.skp, st));
 				TRY(launch_skinny_reduce<false>(b.skp, ks_w2, ks_w2, c.dim, T, c.dim, e, st));
 			} else {
-				TRY(launch_plain(f, bn_w2, b.H, c.hidden_dim, T, c.hidden_dim, c.hidden_dim, one(w.w2, c.dim), c.dim, e,
-				                 st));
+				TRY(launch_plain(f, bn_w2, b.H, sp * c.hidden_dim, T, sp * c.hidden_dim, c.hidden_dim, one(w.w2, c.dim),
+								 c.dim, e, st));
 			}
 		}
 	}
 	if (!want_lp)
 		return YALM_OK;
-	pf::rmsnorm_rows_kernel<false><<<T, 256, 0, st>>>(b.X, d->rms_final, c.dim, c.norm_eps, b.Xn);
+	if (split)
+		pf::rmsnorm_rows_kernel<true><<<T, 256, 0, st>>>(b.X, d->rms_final, c.dim, c.norm_eps, b.Xn,
+                                                         b.range + (size_t)c.n_layers * RG_N + RG_XATT);
+	else
+		pf::rmsnorm_rows_kernel<false><<<T, 256, 0, st>>>(b.X, d->rms_final, c.dim, c.norm_eps, b.Xn,
+                                                          b.range + (size_t)c.n_layers * RG_N + RG_XATT);
 	HIPCHK(hipGetLastError());
 	const int cls_bn = pick_bn(f, PG_CLS, T, c.vocab_size, false);
 	const int ntiles = cls_bn ? c.vocab_size / cls_bn : 1;
@@ -509,7 +593,13 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp) {
 	e.M = T;
 	e.ntiles = ntiles;
 	e.red = nullptr;
-	TRY(launch_plain(f, cls_bn, b.Xn, c.dim, T, c.dim, c.dim, one(d->wcls, c.vocab_size), c.vocab_size, e, st));
+	const void *wcls = d->wcls;
+	if (fp8) {
+		const uint16_t *p[1];
+		TRY(dequant(d, {{d->wcls, (size_t)c.vocab_size * c.dim}}, p, st));
+		wcls = p[0];
+	}
+	TRY(launch_plain(f, cls_bn, b.Xn, sp * c.dim, T, sp * c.dim, c.dim, one(wcls, c.vocab_size), c.vocab_size, e, st));
 	pf::logprob_kernel<<<T, 256, 0, st>>>(b.pmax, b.psum, b.tgt_logit, b.tgt, T, ntiles, b.lp);
 	HIPCHK(hipGetLastError());
 	return YALM_OK;
@@ -547,10 +637,58 @@ extern "C" int yalm_prefill(yalm_decoder d, const int *tokens, int n, int pos0, 
 	}
 	HIPCHK(hipMemcpyAsync(b.tok, tokens, sizeof(int) * n, hipMemcpyHostToDevice, d->stream));
 	HIPCHK(hipMemcpyAsync(b.tgt, tgt.data(), sizeof(int) * n, hipMemcpyHostToDevice, d->stream));
-	TRY(enqueue_prefill(d, n, pos0, logprobs != nullptr));
+	// The range guard (prefill.h range_note): a pass whose f16 operands all fit is the result.
+	// Otherwise the FIRST slot out of range decides (everything after it saw inf / NaN): a GLU
+	// output gets the exact power-of-two scale that brings its largest |h| under 2^14 and the
+	// pass runs again (idempotent: the same cache rows and log-probs are rewritten); any
+	// other operand out of range (the normalised x, Q, the final norm) is refused.
+	const int L = c.n_layers;
+	std::vector<int> hexp(L, 0);
+	std::vector<unsigned> rg((size_t)(L + 1) * RG_N);
+	b.last_passes = b.last_scaled = 0;
+	for (int pass = 1;; ++pass) {
+		HIPCHK(hipMemsetAsync(b.range, 0, rg.size() * 4, d->stream));
+		TRY(enqueue_prefill(d, n, pos0, logprobs != nullptr, hexp.data()));
+		HIPCHK(hipMemcpyAsync(rg.data(), b.range, rg.size() * 4, hipMemcpyDeviceToHost, d->stream));
+		HIPCHK(hipStreamSynchronize(d->stream));
+		b.last_passes = pass;
+		int bad = -1;
+		for (size_t i = 0; i < rg.size() && bad < 0; ++i)
+			if (rg[i])
+				bad = (int)i;
+		if (bad < 0)
+			break;
+		const int l = bad / RG_N, kind = bad % RG_N;
+		float mx;
+		memcpy(&mx, &rg[bad], 4);
+		static const char *what[RG_N] = {"the normalised x (attention input)", "Q", "the normalised x (FFN input)",
+										 "the GLU output"};
+		if (kind != RG_H || l >= L || !std::isfinite(mx) || pass > L + 1) {
+			set_err(std::string("yalm_prefill: ") + (l >= L ? "the final norm's output" : what[kind]) + " of layer " +
+					std::to_string(l) + " exceeds the f16 range of the MFMA operands (max |v| " +
+					std::to_string(mx) + "); the decode path (yalm_forward) keeps it in f32");
+			return YALM_ERR_UNSUPPORTED;
+		}
+		const int e = (int)std::ceil(std::log2(mx / 16384.0f));
+		if (e <= hexp[l]) { // cannot happen for a finite max: a scale that did not help
+			set_err("yalm_prefill: internal: the GLU output scale did not bring layer " + std::to_string(l) + " into range");
+			return YALM_ERR_HIP;
+		}
+		hexp[l] = e;
+	}
+	for (int l = 0; l < L; ++l)
+		b.last_scaled += hexp[l] > 0;
 	if (logprobs)
-		HIPCHK(hipMemcpyAsync(logprobs, b.lp, sizeof(float) * n, hipMemcpyDeviceToHost, d->stream));
-	HIPCHK(hipStreamSynchronize(d->stream));
+		HIPCHK(hipMemcpy(logprobs, b.lp, sizeof(float) * n, hipMemcpyDeviceToHost));
+	return YALM_OK;
+}
+
+extern "C" int yalm_prefill_info(yalm_decoder d, int *passes, int *scaled_layers) {
+	ARGCHK(d, "null decoder");
+	if (passes)
+		*passes = d->pf.last_passes;
+	if (scaled_layers)
+		*scaled_layers = d->pf.last_scaled;
 	return YALM_OK;
 }
 

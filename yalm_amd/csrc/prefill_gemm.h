@@ -93,11 +93,12 @@ struct E16StoreF32 {
 	}
 };
 
-struct E16Residual { // X[m][n] += C  (fused_matmul_add_residuals, per row)
+struct E16Residual { // X[m][n] += scale C  (fused_matmul_add_residuals, per row)
 	static constexpr bool NEEDS_LDS = false;
 	float *red = nullptr;
 	float *x;
 	int ldx, M;
+	float scale = 1.0f; // 2^e: undoes the exact power-of-two scale of an f16 A operand (E16Glu::hscale)
 	// per row fragment: all 4 FJ loads of x issued (rows clamped) before any add, the stores
 	// predicated on the row (a per-element branch around the load made hipcc wait for each
 	// load separately: E16QKV below)
@@ -119,7 +120,7 @@ struct E16Residual { // X[m][n] += C  (fused_matmul_add_residuals, per row)
 				if (m < M)
 #pragma unroll
 					for (int j = 0; j < FJ; ++j)
-						x[(size_t)m * ldx + n0 + 16 * j + (lane & 15)] = xv[r][j] + acc[i][j][r];
+						x[(size_t)m * ldx + n0 + 16 * j + (lane & 15)] = xv[r][j] + acc[i][j][r] * scale;
 			}
 		}
 	}
@@ -145,14 +146,22 @@ __device__ __forceinline__ float act_fast(float x) {
 // H = f16(act(X W1^T) * (X W3^T)) (fused_ffn_w1_w3_glu_act): columns j < FJ / 2 of a
 // wave are W1 outputs, j >= FJ / 2 the W3 outputs of the same hidden columns.
 // n0 here is the wave's first HIDDEN column (BRowsGlu).
+// hscale: an exact power of two 2^-e (default 1) applied before the f16 rounding when the
+// layer's GLU products exceed the f16 range (prefill.hip: found by range_note, the pass
+// re-run with the scale, the W2 epilogue multiplying by 2^e); values below 2^-14 * 2^e then
+// lose relative precision as f16 subnormals, far under the W2 sum's own rounding.
 template <int ACT>
 struct E16Glu {
 	static constexpr bool NEEDS_LDS = false;
 	float *red = nullptr;
 	uint16_t *h;
 	int ldh, M;
+	float hscale = 1.0f;
+	unsigned *range = nullptr;
+	int lo_off = 0; // split-operand form: f16(v - hi) stored lo_off columns after hi (H rows [hi | lo])
 	template <int FI, int FJ>
 	__device__ __forceinline__ void apply(f32x4_t (&acc)[FI][FJ], int m0, int n0, int lane, int, int) const {
+		float vmax = 0.0f;
 #pragma unroll
 		for (int i = 0; i < FI; ++i)
 #pragma unroll
@@ -161,10 +170,18 @@ struct E16Glu {
 				if (m >= M)
 					continue;
 #pragma unroll
-				for (int j = 0; j < FJ / 2; ++j)
-					h[(size_t)m * ldh + n0 + 16 * j + (lane & 15)] =
-					    f2h_bits(act_fast<ACT>(acc[i][j][r]) * acc[i][j + FJ / 2][r]);
+				for (int j = 0; j < FJ / 2; ++j) {
+					const float v = act_fast<ACT>(acc[i][j][r]) * acc[i][j + FJ / 2][r];
+					vmax = fmaxf(vmax, v != v ? __builtin_inff() : fabsf(v)); // NaN counts as inf
+					const float vs = v * hscale;
+					const uint16_t hb = f2h_bits(vs);
+					uint16_t *const hp = h + (size_t)m * ldh + n0 + 16 * j + (lane & 15);
+					hp[0] = hb;
+					if (lo_off)
+						hp[lo_off] = f2h_bits(vs - h2f(hb));
+				}
 			}
+		range_note(range, vmax * hscale, vmax);
 	}
 };
 
@@ -184,9 +201,13 @@ struct E16QKV {
 	const float *rope;
 	int M, q_dim, kv_dim, head_dim, pos0;
 	float clip;
+	unsigned *range = nullptr; // the f16 Q operand out of range (range_note); K / V are the
+							   // f16 cache rows of the reference too (infer.cpp:299)
+	int q_lo = 0;              // split-operand form: Q rows [hi | lo], lo q_lo columns after hi
 	template <int FI, int FJ>
 	__device__ __forceinline__ void apply(f32x4_t (&acc)[FI][FJ], int m0, int n0, int lane, int, int) const {
 		const bool odd = lane & 1;
+		float qmax = 0.0f;
 #pragma unroll
 		for (int j = 0; j < FJ; ++j) {
 			const int nb = __builtin_amdgcn_readfirstlane(n0 + 16 * j); // block's first column
@@ -196,7 +217,7 @@ struct E16QKV {
 			const int fj = (nn % head_dim) >> 1;
 			const bool rot = region != 2;
 			uint16_t *const dst = (region == 0 ? q : (region == 1 ? kc : vc)) + nn;
-			const int ld = region == 0 ? q_dim : kv_dim, roff = region == 0 ? 0 : pos0;
+			const int ld = region == 0 ? q_dim + q_lo : kv_dim, roff = region == 0 ? 0 : pos0;
 			constexpr int IB = FI < 4 ? FI : 4; // row fragments per batch of table loads
 #pragma unroll
 			for (int i0 = 0; i0 < FI; i0 += IB) {
@@ -217,11 +238,19 @@ struct E16QKV {
 						const float p = dpp<0xB1>(v); // partner column (n ^ 1)
 						const float ro = odd ? p * cs[i][r][1] + v * cs[i][r][0] : v * cs[i][r][0] - p * cs[i][r][1];
 						const int m = m0 + 16 * (i0 + i) + crow16(r, lane);
-						if (m < M)
-							dst[(size_t)(roff + m) * ld] = f2h(rot ? ro : v);
+						const float o = rot ? ro : v;
+						if (region == 0 && m < M)
+							qmax = fmaxf(qmax, o != o ? __builtin_inff() : fabsf(o));
+						if (m < M) {
+							const uint16_t ob = f2h(o);
+							dst[(size_t)(roff + m) * ld] = ob;
+							if (region == 0 && q_lo)
+								dst[(size_t)m * ld + q_lo] = f2h(o - h2f(ob));
+						}
 					}
 			}
 		}
+		range_note(range, qmax, qmax);
 	}
 };
 

@@ -96,6 +96,38 @@ extern "C" int yalm_stream_create(yalm_stream *out) {
 	return YALM_OK;
 }
 
+// A stream restricted to CU block `part` of `n_parts` (hipExtStreamCreateWithCUMask):
+// bits [part * ncu / n_parts, (part + 1) * ncu / n_parts). The driver spreads such a block
+// evenly over the 8 XCDs (tools/cumask_probe.hip, profiles/r6a_cumask_probe.txt: 256 / N CUs
+// on all 8 XCCs, disjoint between parts); an interleaved mask (bit i to part i mod N) was
+// not honoured (every part ran on all 256 CUs). Used to run N tensor-parallel rank
+// processes on ONE GPU as N disjoint sets of CUs (the multi-GPU rehearsal).
+extern "C" int yalm_stream_create_cu_part(int part, int n_parts, yalm_stream *out) {
+	ARGCHK(out && n_parts >= 1 && part >= 0 && part < n_parts, "yalm_stream_create_cu_part: bad argument");
+	const int ncu = device_cu_count();
+	ARGCHK(ncu % n_parts == 0 && ncu <= 32 * YALM_CU_MASK_WORDS, "yalm_stream_create_cu_part: CUs do not divide");
+	uint32_t m[YALM_CU_MASK_WORDS] = {};
+	for (int i = part * (ncu / n_parts); i < (part + 1) * (ncu / n_parts); ++i)
+		m[i / 32] |= 1u << (i % 32);
+	hipStream_t s;
+	HIPCHK(hipExtStreamCreateWithCUMask(&s, (uint32_t)((ncu + 31) / 32), m));
+	*out = reinterpret_cast<yalm_stream>(s);
+	return YALM_OK;
+}
+
+// The CUs a stream may run on (all of them for an ordinary stream).
+static int stream_cu_mask(hipStream_t s, uint32_t *m) {
+	const int ncu = device_cu_count();
+	for (int i = 0; i < YALM_CU_MASK_WORDS; ++i)
+		m[i] = 0;
+	if (!s || hipExtStreamGetCUMask(s, (uint32_t)((ncu + 31) / 32), m) != hipSuccess) {
+		(void)hipGetLastError();
+		for (int i = 0; i < ncu && i < 32 * YALM_CU_MASK_WORDS; ++i)
+			m[i / 32] |= 1u << (i % 32);
+	}
+	return YALM_OK;
+}
+
 extern "C" int yalm_stream_destroy(yalm_stream s) {
 	HIPCHK(hipStreamDestroy(reinterpret_cast<hipStream_t>(s)));
 	return YALM_OK;
@@ -419,9 +451,6 @@ extern "C" int yalm_attn_wo_plan(const yalm_config *cp, int slots, int *splits, 
 // partial for the all-reduce (RCCL) or push it to the exchange (IPC, tp_exchange.h).
 static int attn_wo_init(yalm_decoder_s *d) {
 	const yalm_config &c = d->c;
-	const char *env = getenv("YALM_ATTN_WO");
-	if (env && atoi(env) == 0)
-		return YALM_OK;
 	if (c.head_dim != 128)
 		return YALM_OK;
 	const int G = c.n_heads / c.n_kv_heads;
@@ -454,7 +483,7 @@ static int attn_wo_init(yalm_decoder_s *d) {
 	const char *tenv = ab_env("YALM_ATTN_WO_TRACE");
 	if (tenv && atoi(tenv) != 0)
 		TRY(dalloc(d, (void **)&d->awo_trace, sizeof(unsigned long long) * AWO_TRACE_N * d->awo_nb));
-	d->attn_wo = true;
+	d->attn_wo = d->attn_wo_ok = true;
 	return YALM_OK;
 }
 
@@ -471,7 +500,7 @@ int awo_check(yalm_decoder_s *d) {
 			std::string m = "bounded in-launch wait gave up (results invalid):";
 			if (e & 1u)
 				m += " the fused attention + Wo launch's Wo gather timed out waiting for the attention heads"
-				     " (YALM_ATTN_WO=0 selects separate launches);";
+				     " (yalm_decoder_set_launch YALM_LAUNCH_SEPARATE_ATTN_WO selects separate launches);";
 			if (e & 2u)
 				m += " the split-KV attention merger timed out waiting for a key-chunk partial;";
 			if (e & ~3u)
@@ -928,8 +957,6 @@ static int create_decoder(const yalm_config *config, const yalm_model_weights *w
 	const int nsplit = attn_nsplit(c.max_seq_len);
 	d->tokens_cap = 1 << 16;
 	d->pf_forms = pf_forms_default();
-	d->eager = getenv("YALM_EAGER") && atoi(getenv("YALM_EAGER")) != 0;
-	d->graph_sync = getenv("YALM_GRAPH_SYNC") && atoi(getenv("YALM_GRAPH_SYNC")) != 0;
 	{
 		const char *g = ab_env("YALM_GREEDY_GRAPH");
 		d->greedy_eager = !(g && atoi(g) != 0);
@@ -1057,15 +1084,39 @@ extern "C" int yalm_decoder_create_tp(const yalm_config *config, const yalm_mode
 	return r;
 }
 
-extern "C" int yalm_tp_ipc_alloc(const yalm_config *config, int tp_size, void **buf, void *handle_out) {
+// The rank record every rank shares (YALM_TP_HANDLE_BYTES): the IPC handle of its exchange
+// buffer, then WHERE the rank runs -- its GPU's UUID and the CU mask of its decoder stream.
+// Two ranks contend for compute only when both match (same GPU, overlapping CUs): ADVICE r5
+// (medium) -- the round-5 test compared hipPointerGetAttributes(peer mapping).device with the
+// current device, which an IPC-imported mapping need not report as the exporter's.
+struct TpRankRecord {
+	unsigned char ipc[64];
+	unsigned char uuid[16];
+	uint32_t cu_mask[YALM_CU_MASK_WORDS];
+	unsigned char reserved[YALM_TP_HANDLE_BYTES - 64 - 16 - 4 * YALM_CU_MASK_WORDS];
+};
+static_assert(sizeof(TpRankRecord) == YALM_TP_HANDLE_BYTES, "rank record size");
+static_assert(sizeof(hipIpcMemHandle_t) == 64, "IPC handle size");
+
+extern "C" int yalm_tp_ipc_alloc(const yalm_config *config, int tp_size, yalm_stream s, void **buf,
+                                 void *handle_out) {
 	ARGCHK(config && buf && handle_out && tp_size >= 1 && tp_size <= 8, "yalm_tp_ipc_alloc: bad argument (1..8 ranks)");
 	const size_t bytes = ipc_buf_bytes(*config, tp_size);
 	// uncached (tp_exchange.h): peers push into it, so no reader's L2 may hold a stale line
 	HIPCHK(hipExtMallocWithFlags(buf, bytes, hipDeviceMallocUncached));
 	HIPCHK(hipMemset(*buf, 0, bytes));
+	TpRankRecord rec;
+	memset(&rec, 0, sizeof(rec));
 	hipIpcMemHandle_t h;
 	HIPCHK(hipIpcGetMemHandle(&h, *buf));
-	memcpy(handle_out, &h, sizeof(h));
+	memcpy(rec.ipc, &h, sizeof(h));
+	int dev = 0;
+	HIPCHK(hipGetDevice(&dev));
+	hipUUID u;
+	HIPCHK(hipDeviceGetUuid(&u, dev));
+	memcpy(rec.uuid, &u, sizeof(rec.uuid));
+	TRY(stream_cu_mask(reinterpret_cast<hipStream_t>(s), rec.cu_mask));
+	memcpy(handle_out, &rec, sizeof(rec));
 	HIPCHK(hipDeviceSynchronize());
 	return YALM_OK;
 }
@@ -1079,6 +1130,14 @@ extern "C" int yalm_decoder_create_tp_ipc(const yalm_config *config, const yalm_
 	TRY(tp_local_config(*config, tp_size, lc));
 	ARGCHK(config->dim % (64 * (config->weight_dtype == YALM_F32 ? 4 : config->weight_dtype == YALM_F16 ? 8 : 16)) == 0,
 	       "tensor parallel (IPC): dim must be a multiple of 64 x the elements of a 16-byte load");
+	std::vector<TpRankRecord> recs(tp_size);
+	memcpy(recs.data(), handles, sizeof(TpRankRecord) * tp_size);
+	{ // this rank's record must describe the stream it decodes on
+		uint32_t m[YALM_CU_MASK_WORDS];
+		TRY(stream_cu_mask(reinterpret_cast<hipStream_t>(s), m));
+		ARGCHK(!memcmp(m, recs[tp_rank].cu_mask, sizeof(m)),
+		       "yalm_decoder_create_tp_ipc: this rank's record was made for another stream (CU mask differs)");
+	}
 	std::vector<float *> bases(tp_size);
 	std::vector<void *> opened;
 	for (int p = 0; p < tp_size; ++p) {
@@ -1087,7 +1146,7 @@ extern "C" int yalm_decoder_create_tp_ipc(const yalm_config *config, const yalm_
 			continue;
 		}
 		hipIpcMemHandle_t h;
-		memcpy(&h, (const char *)handles + (size_t)p * sizeof(h), sizeof(h));
+		memcpy(&h, recs[p].ipc, sizeof(h));
 		void *ptr = nullptr;
 		if (hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
 			for (void *q : opened)
@@ -1118,21 +1177,26 @@ extern "C" int yalm_decoder_create_tp_ipc(const yalm_config *config, const yalm_
 		return YALM_ERR_HIP;
 	}
 	d->ipc_bufs = (float **)dev_bases;
-	int dev = 0;
-	HIPCHK(hipGetDevice(&dev));
-	for (int p = 0; p < tp_size; ++p) { // a peer's buffer on this device: ranks share the GPU
-		hipPointerAttribute_t at;
-		if (p != tp_rank && hipPointerGetAttributes(&at, bases[p]) == hipSuccess && at.device == dev)
-			d->tpx_gate = true;
+	// Ranks whose kernels can hold each other's CUs: the same GPU (UUID) with overlapping CU
+	// masks (several rank processes on one GPU without yalm_stream_create_cu_part). One GPU
+	// per rank -- or disjoint CU masks on one GPU, the rehearsal of that -- needs no gate.
+	for (int p = 0; p < tp_size; ++p) {
+		if (p == tp_rank || memcmp(recs[p].uuid, recs[tp_rank].uuid, sizeof(recs[p].uuid)))
+			continue;
+		for (int i = 0; i < YALM_CU_MASK_WORDS; ++i)
+			if (recs[p].cu_mask[i] & recs[tp_rank].cu_mask[i])
+				d->tpx_gate = true;
 	}
 	// The fused attention + Wo launch's Wo workgroups spin on attention workgroups of the
-	// same launch, which is deadlock-free while the grid is co-resident. Ranks sharing one
-	// GPU launch their grids concurrently; when they cannot all be resident at once, a
-	// workgroup dispatched on a full XCD can trail Wo workgroups already spinning on other
-	// XCDs (measured: TP8 at Mistral dims, 8 processes on one MI355X, the Wo gather timed
-	// out). Those ranks keep the separate attention and Wo launches.
+	// same launch; a workgroup only ever waits on lower-index ones, and each XCD dispatches
+	// its workgroups in index order, so by induction on the index every workgroup is
+	// dispatched and finishes whatever fits at once (on a CU-masked rehearsal stream the
+	// production grid runs in several rounds: correct, just slower). Ranks whose grids SHARE
+	// CUs break that: a workgroup dispatched on a full XCD can trail another rank's Wo
+	// workgroups spinning there (measured: TP8 at Mistral dims, 8 unmasked processes on one
+	// MI355X, the Wo gather timed out). Those ranks keep the separate attention and Wo launches.
 	if (d->tpx_gate && d->attn_wo && d->awo_nb * tp_size > d->awo_slots)
-		d->attn_wo = false;
+		d->attn_wo = d->attn_wo_ok = false;
 	d->tpx_collect = tp_size > TPX_STAGE_MAX_RANKS;
 	d->tpx.bufs = d->ipc_bufs;
 	d->tpx.rank = tp_rank;
@@ -1350,7 +1414,7 @@ static int enqueue_one_t(yalm_decoder_s *d, int kernel_id, int l) {
 
 extern "C" int yalm_graph_kernels(yalm_decoder d, int mode, int *kernels, int *nodes) {
 	ARGCHK(d && kernels && mode >= 0 && mode < N_GRAPHS, "yalm_graph_kernels: bad argument");
-	ARGCHK(!d->eager, "yalm_graph_kernels: the decoder launches eagerly (YALM_EAGER)");
+	ARGCHK(!d->eager, "yalm_graph_kernels: the decoder launches eagerly (YALM_LAUNCH_EAGER)");
 	TRY(ensure_graph(d, mode));
 	size_t n = 0;
 	HIPCHK(hipGraphGetNodes(d->graph[mode], nullptr, &n));
@@ -1366,6 +1430,17 @@ extern "C" int yalm_graph_kernels(yalm_decoder d, int mode, int *kernels, int *n
 	*kernels = k;
 	if (nodes)
 		*nodes = (int)n;
+	return YALM_OK;
+}
+
+extern "C" int yalm_decoder_set_launch(yalm_decoder d, int flags) {
+	ARGCHK(d, "null decoder");
+	ARGCHK(!(flags & ~(YALM_LAUNCH_EAGER | YALM_LAUNCH_SYNC | YALM_LAUNCH_SEPARATE_ATTN_WO)), "unknown launch flag");
+	HIPCHK(hipStreamSynchronize(d->stream));
+	drop_graphs(d); // captured graphs bake the old launch sequence
+	d->eager = flags & YALM_LAUNCH_EAGER;
+	d->graph_sync = flags & YALM_LAUNCH_SYNC;
+	d->attn_wo = d->attn_wo_ok && !(flags & YALM_LAUNCH_SEPARATE_ATTN_WO);
 	return YALM_OK;
 }
 
@@ -1422,6 +1497,11 @@ extern "C" int yalm_time_kernel(yalm_decoder d, int kernel_id, int iters, float 
 	ARGCHK(kernel_id != 8 || d->attn_wo, "kernel 8 (fused attention + Wo) needs yalm_decoder_attn_wo");
 	// in-launch hand-offs and the IPC exchange: fresh tags per launch (one exchange per bump)
 	const bool bump = kernel_id == 1 || kernel_id == 8 || (kernel_id == 6 && d->ipc);
+	// the warm-up gets a fresh epoch too: under IPC it pushes exchange xbase + 0, whose slot
+	// parity the previous forward's argmax exchange (2 L, even) used -- without the bump a
+	// peer still reading that slot could see it overwritten (tp_exchange.h reuse rule)
+	if (bump)
+		epoch_bump_kernel<<<1, 1, 0, d->stream>>>(d->step, 1);
 	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_one_t, d, kernel_id, 0)); // warm-up
 	float ms = 0.f;
 	TRY(time_loop(d, kernel_id, iters, bump, true, &ms));

@@ -175,7 +175,11 @@ static void run_perplexity(const std::string &path, const std::string &device, c
 	size_t pos = 0;
 	const size_t B = std::min(encoding.size(), (size_t)model.config->max_seq_len);
 	std::vector<float> lps(B);
-	if (B >= 2 && model.prefill(state, encoding.data(), (int)B, 0, lps.data())) {
+	// the split-operand precision form: every activation operand carries the f32 the
+	// reference keeps to ~2^-22, so the perplexity is the reference's; a
+	// model whose activations do not fit the prefill's operands (YALM_ERR_UNSUPPORTED) runs
+	// position by position below, as the reference does
+	if (B >= 2 && model.prefill(state, encoding.data(), (int)B, 0, lps.data(), true)) {
 		for (; pos + 1 < B; ++pos) {
 			const double lp = lps[pos];
 			sum_logprob += lp;

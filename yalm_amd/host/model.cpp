@@ -262,11 +262,12 @@ void Model::forward(InferenceState &s, int token, int pos, InferenceMode mode) {
 	      "forward");
 }
 
-bool Model::prefill(InferenceState &s, const int *tokens, int n, int pos0, float *logprobs) {
+bool Model::prefill(InferenceState &s, const int *tokens, int n, int pos0, float *logprobs, bool split) {
 	const char *off = getenv("YALM_NO_PREFILL");
 	if ((off && atoi(off) != 0) || n <= 0)
 		return false;
 	ensure_decoder(s);
+	check(yalm_set_prefill_precision(s._decoder, split ? YALM_PREFILL_SPLIT : YALM_PREFILL_FAST), "prefill precision");
 	const int r = yalm_prefill(s._decoder, tokens, n, pos0, logprobs);
 	if (r == YALM_ERR_UNSUPPORTED)
 		return false;

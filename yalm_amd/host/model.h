@@ -124,10 +124,12 @@ struct Model {
 	int forward_greedy(InferenceState &s, int token, int pos);
 	// Batched MFMA prefill of tokens[0..n) at positions pos0.. (yalm_prefill):
 	// fills the KV cache; logprobs (may be null) gets log p(tokens[i+1]) per
-	// position. Returns false when this model's shape/dtype has no prefill
-	// path (f16 weights, dims multiple of 128, head_dim 64|128) or
-	// YALM_NO_PREFILL=1; the caller then runs the per-position forward.
-	bool prefill(InferenceState &s, const int *tokens, int n, int pos0, float *logprobs);
+	// position; split: the split-operand precision form (yalm_set_prefill_precision).
+	// Returns false when this model's shape/dtype has no prefill path (f16 / fp8
+	// weights, dims multiple of 128, head_dim 64|128), its activations leave the
+	// prefill's f16 operand range, or YALM_NO_PREFILL=1; the caller then runs the
+	// per-position forward.
+	bool prefill(InferenceState &s, const int *tokens, int n, int pos0, float *logprobs, bool split = false);
 	void cuda(); // Model::cuda (model.cpp:380-394)
 	void hip() {
 		cuda();

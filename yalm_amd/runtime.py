@@ -118,10 +118,14 @@ _sig("yalm_ffn", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int
 _sig("yalm_prefill", c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p])
 _sig("yalm_tp_unique_id", c_int, [c_void_p])
 _sig("yalm_decoder_create_tp", c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p])
-_sig("yalm_tp_ipc_alloc", c_int, [c_void_p, c_int, ctypes.POINTER(c_void_p), c_void_p])
+_sig("yalm_tp_ipc_alloc", c_int, [c_void_p, c_int, c_void_p, ctypes.POINTER(c_void_p), c_void_p])
+_sig("yalm_stream_create_cu_part", c_int, [c_int, c_int, ctypes.POINTER(c_void_p)])
+_sig("yalm_decoder_set_launch", c_int, [c_void_p, c_int])
 _sig("yalm_decoder_create_tp_ipc", c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p])
 _sig("yalm_copy_2d", c_int, [c_void_p, ctypes.c_size_t, c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t])
 _sig("yalm_prefill_time", c_int, [c_void_p, c_int, c_int, ctypes.POINTER(c_float)])
+_sig("yalm_prefill_info", c_int, [c_void_p, ctypes.POINTER(c_int), ctypes.POINTER(c_int)])
+_sig("yalm_set_prefill_precision", c_int, [c_void_p, c_int])
 _sig("yalm_gemm_f16", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int])
 _sig("yalm_attn_prefill", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int])
 _sig("yalm_set_prefill_forms", c_int, [c_void_p, ctypes.c_char_p])
@@ -138,9 +142,14 @@ EXPORTED = [
     "yalm_decoder_create_tp", "yalm_copy_2d", "yalm_tp_ipc_alloc", "yalm_decoder_create_tp_ipc",
     "yalm_decoder_attn_wo", "yalm_attn_wo_trace", "yalm_stream_envelope",
     "yalm_argmax", "yalm_set_prefill_forms", "yalm_attn_wo_plan", "yalm_graph_kernels",
+    "yalm_stream_create_cu_part", "yalm_decoder_set_launch", "yalm_prefill_info", "yalm_set_prefill_precision",
 ]
+PREFILL_FAST, PREFILL_SPLIT = 0, 1  # yalm_set_prefill_precision
 
 HYDRATE_KV_CACHE, OUTPUT_LOGITS = 0, 1
+# yalm_decoder_set_launch flags (include/yalm_hip.h)
+LAUNCH_EAGER, LAUNCH_SYNC, LAUNCH_SEPARATE_ATTN_WO = 1, 2, 4
+TP_HANDLE_BYTES = 128  # YALM_TP_HANDLE_BYTES: IPC handle + GPU UUID + CU mask
 
 
 class YalmError(RuntimeError):
@@ -204,6 +213,24 @@ def stream_envelope(nbytes: int, iters: int = 16) -> float:
     ms = c_float()
     check(lib.yalm_stream_envelope(nbytes, iters, ctypes.byref(ms)))
     return ms.value
+
+
+class Stream:
+    """A decoder stream; cu_part = (part, n_parts): restricted to CU block `part` of
+    n_parts (yalm_stream_create_cu_part), so n_parts rank processes on one GPU run on
+    disjoint CUs -- the one-GPU rehearsal of tensor parallelism."""
+
+    def __init__(self, cu_part=None):
+        self.h = c_void_p()
+        if cu_part is None:
+            check(lib.yalm_stream_create(ctypes.byref(self.h)))
+        else:
+            check(lib.yalm_stream_create_cu_part(cu_part[0], cu_part[1], ctypes.byref(self.h)))
+
+    def close(self):
+        if self.h:
+            check(lib.yalm_stream_destroy(self.h))
+            self.h = None
 
 
 def tp_unique_id() -> bytes:
@@ -301,14 +328,19 @@ class DeviceModel:
             yd.close()
 
     @classmethod
-    def synthetic(cls, cfg: M.ModelConfig, seed: int = 1, tp=(0, 1), peak: float = 1.0) -> "DeviceModel":
+    def synthetic(cls, cfg: M.ModelConfig, seed: int = 1, tp=(0, 1), peak: float = 1.0,
+                  real: "M.Realistic" = None) -> "DeviceModel":
         """Random-weight model of cfg's shape generated directly in HBM with the
         deterministic hash shared with the oracle (no PCIe upload). tp = (rank,
         size): keep only this rank's shards — each sharded tensor is generated
         whole in a scratch buffer and its slice copied out (yalm_copy_2d), so
-        every rank holds exactly the slices of the same full model."""
+        every rank holds exactly the slices of the same full model. real: the
+        realistic model (models.Realistic): each patched tensor is downloaded, patched
+        by models.realistic_patch and uploaded again (single GPU only)."""
         rank, size = tp
         M.tp_check(cfg, size)
+        if real is not None and size > 1:
+            raise ValueError("the realistic synthetic model is built for one GPU (tp size 1)")
         self = cls(cfg)
         self.tp = tp
         names = list(M.tensor_shapes(cfg).items())
@@ -319,7 +351,7 @@ class DeviceModel:
             dt = M.F32 if is_norm else cfg.weight_dtype
             eb = M.DTYPE_BYTES[dt]
             src_name = "model.embed.weight" if name == "tp.wcls" else name
-            scale, offset = M.synth_params(src_name, is_norm, peak)
+            scale, offset = M.synth_params(src_name, is_norm, peak, real)
             sh = M.tp_shard(cfg, name, rank, size)
             if sh is None:
                 p = self._alloc(n * eb)
@@ -343,6 +375,21 @@ class DeviceModel:
                     lib.yalm_free(full)
             self.ptrs[name] = p
         check(lib.yalm_stream_sync(None))
+        if real is not None:
+            shapes = M.tensor_shapes(cfg)
+            for name in M.realistic_names(cfg):
+                shape, is_norm = shapes[name]
+                dt = M.F32 if is_norm else cfg.weight_dtype
+                a = np.empty(shape, {M.F32: np.float32, M.F16: np.float16, M.F8E5M2: np.uint8}[dt])
+                check(lib.yalm_download(a.ctypes.data, self.ptrs[name], a.nbytes))
+                M.realistic_patch(cfg, name, a, real)
+                p = lib.yalm_upload(a.ctypes.data, a.nbytes)
+                if not p:
+                    raise YalmError(lib.yalm_last_error().decode())
+                old = self.ptrs[name]
+                self._owned[self._owned.index(old)] = p
+                lib.yalm_free(old)
+                self.ptrs[name] = p
         return self
 
     def weights_struct(self):
@@ -367,16 +414,19 @@ class DeviceModel:
 class Decoder:
     """InferenceState on the device + Model::forward (graph-replayed)."""
 
-    def __init__(self, model: DeviceModel, tp_id: bytes = None, tp_gather=None, kv_caches=None):
+    def __init__(self, model: DeviceModel, tp_id: bytes = None, tp_gather=None, kv_caches=None,
+                 cu_part=None, launch: int = 0):
         """Tensor parallel over model.tp = (rank, size), one of:
         tp_id: the RCCL unique id (tp_unique_id() on rank 0, shared with the
-        other ranks); tp_gather: a function mapping this rank's 64-byte IPC
-        handle to the list of every rank's handle (e.g. via
-        torch.distributed.all_gather_object) for the IPC exchange transport.
+        other ranks); tp_gather: a function mapping this rank's 128-byte rank
+        record (IPC handle, GPU UUID, CU mask) to the list of every rank's record
+        (e.g. via torch.distributed.all_gather_object) for the IPC exchange transport.
         Neither: a single-GPU decoder. kv_caches: optional per-layer (key, value)
         device pointers ([max_seq_len][kv_dim] f16 each, caller-owned), as
         Block::cuda() hands its own caches over (model.cpp:185-211); default: the
-        decoder allocates zeroed caches."""
+        decoder allocates zeroed caches. cu_part = (part, n_parts): decode on a
+        stream restricted to that CU block (Stream). launch: yalm_decoder_set_launch
+        flags (LAUNCH_*)."""
         self.model = model
         self.cfg = model.cfg
         self._c = Config.from_model(self.cfg)
@@ -386,25 +436,34 @@ class Decoder:
                 self._blocks[l].key_cache = kp
                 self._blocks[l].value_cache = vp
         self._mw = mw
+        self.h = None
+        self.stream = Stream(cu_part) if cu_part is not None else None
+        sh = self.stream.h if self.stream else None
         h = c_void_p()
         if tp_gather is not None:
             rank, size = getattr(model, "tp", (0, 1))
             buf = c_void_p()
-            handle = ctypes.create_string_buffer(64)
-            check(lib.yalm_tp_ipc_alloc(ctypes.byref(self._c), size, ctypes.byref(buf), handle))
+            handle = ctypes.create_string_buffer(TP_HANDLE_BYTES)
+            check(lib.yalm_tp_ipc_alloc(ctypes.byref(self._c), size, sh, ctypes.byref(buf), handle))
             handles = tp_gather(handle.raw)
-            assert len(handles) == size and all(len(x) == 64 for x in handles)
-            hb = ctypes.create_string_buffer(b"".join(handles), 64 * size)
-            check(lib.yalm_decoder_create_tp_ipc(ctypes.byref(self._c), ctypes.byref(mw), rank, size, buf, hb, None,
+            assert len(handles) == size and all(len(x) == TP_HANDLE_BYTES for x in handles)
+            hb = ctypes.create_string_buffer(b"".join(handles), TP_HANDLE_BYTES * size)
+            check(lib.yalm_decoder_create_tp_ipc(ctypes.byref(self._c), ctypes.byref(mw), rank, size, buf, hb, sh,
                                                  ctypes.byref(h)))
         elif tp_id is None:
-            check(lib.yalm_decoder_create(ctypes.byref(self._c), ctypes.byref(mw), None, ctypes.byref(h)))
+            check(lib.yalm_decoder_create(ctypes.byref(self._c), ctypes.byref(mw), sh, ctypes.byref(h)))
         else:
             rank, size = getattr(model, "tp", (0, 1))
             idb = ctypes.create_string_buffer(bytes(tp_id), 128)
-            check(lib.yalm_decoder_create_tp(ctypes.byref(self._c), ctypes.byref(mw), rank, size, idb, None,
+            check(lib.yalm_decoder_create_tp(ctypes.byref(self._c), ctypes.byref(mw), rank, size, idb, sh,
                                              ctypes.byref(h)))
         self.h = h
+        if launch:
+            self.set_launch(launch)
+
+    def set_launch(self, flags: int) -> None:
+        """yalm_decoder_set_launch: LAUNCH_EAGER | LAUNCH_SYNC | LAUNCH_SEPARATE_ATTN_WO (0 = default)."""
+        check(lib.yalm_decoder_set_launch(self.h, flags))
 
     def forward(self, token: int, pos: int, mode: int = OUTPUT_LOGITS):
         if mode == OUTPUT_LOGITS:
@@ -421,6 +480,16 @@ class Decoder:
         out = np.zeros(len(tok), np.float32) if logprobs else None
         check(lib.yalm_prefill(self.h, _ptr(tok), len(tok), pos0, _ptr(out) if logprobs else None))
         return out
+
+    def set_prefill_precision(self, mode: int) -> None:
+        """PREFILL_FAST (f16 activation operands) or PREFILL_SPLIT (every operand [hi | lo])."""
+        check(lib.yalm_set_prefill_precision(self.h, mode))
+
+    def prefill_info(self):
+        """(passes, scaled layers) of the last prefill: the f16 range guard's re-runs."""
+        p, n = c_int(), c_int()
+        check(lib.yalm_prefill_info(self.h, ctypes.byref(p), ctypes.byref(n)))
+        return p.value, n.value
 
     def set_prefill_forms(self, spec: str = "") -> None:
         """Select another exact prefill GEMM form (yalm_set_prefill_forms), "" = defaults."""
@@ -502,6 +571,9 @@ class Decoder:
         if self.h:
             check(lib.yalm_decoder_destroy(self.h))
             self.h = None
+        if getattr(self, "stream", None) is not None:
+            self.stream.close()
+            self.stream = None
 
     def __del__(self):
         try:
