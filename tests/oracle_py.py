@@ -129,7 +129,7 @@ def synth_host_tensors_fast(cfg: M.ModelConfig, seed: int = 1, peak: float = 1.0
     out = {}
     for name, (shape, is_norm) in M.tensor_shapes(cfg).items():
         n = int(np.prod(shape))
-        scale, offset = M.synth_params(name, is_norm, peak, real)
+        scale, offset = M.synth_params(name, is_norm, peak, real, cfg.tied)
         s = M.synth_seed(seed, name)
         if is_norm:
             a = np.empty(n, np.float32)

@@ -59,9 +59,10 @@ def test_mistral_config2_256_tokens_vs_oracle(real):
 
     realistic (round 5's "peaked" model only scaled the final norm by 2^3,
     an exact logit scale that could not change a token): models.REALISTIC, hidden states with
-    a trained checkpoint's regimes -- peaked attention softmax (Wq / Wk x 12), three residual
+    a trained checkpoint's regimes -- peaked attention softmax (Wq / Wk x 24), three residual
     outlier channels of 10^2..10^3 (embedding columns, W2 rows), a GLU product above 65504 at
-    every position in layer 1, a final norm x 0.7; next-token distributions peaked (top-1
+    every position in layer 1, a final norm x 4.5, a residual stream that dominates its
+    branches (not chaotic: models.Realistic); next-token distributions peaked (top-1
     probability >= 0.5 at most steps, log ppl of the greedy text << ln(vocab)). The default
     synthetic model's are near-uniform (logit std ~1.2)."""
     from yalm_amd import runtime

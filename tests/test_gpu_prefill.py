@@ -264,16 +264,26 @@ def test_fp8_prefill_equals_f16_twin(cfg_name, n):
     cfg16, t16 = _f16_twin(cfg8, t8)
     R = rt()
     dm8, dm16 = R.DeviceModel.from_arrays(cfg8, t8), R.DeviceModel.from_arrays(cfg16, t16)
-    d8, d16, dd = R.Decoder(dm8), R.Decoder(dm16), R.Decoder(dm8)
+    kvb = cfg8.max_seq_len * cfg8.kv_dim * 2
+    caches = [[R.lib.yalm_alloc(kvb) for _ in range(2 * cfg8.n_layers)] for _ in range(2)]  # caller-owned K / V
+    d8 = R.Decoder(dm8, kv_caches=list(zip(caches[0][0::2], caches[0][1::2])))
+    d16 = R.Decoder(dm16, kv_caches=list(zip(caches[1][0::2], caches[1][1::2])))
+    dd = R.Decoder(dm8)
     try:
         tokens = np.random.default_rng(31 + n).integers(0, cfg8.vocab_size, size=n).astype(np.int32)
         lp8, lp16 = d8.prefill(tokens), d16.prefill(tokens)
         np.testing.assert_array_equal(lp8, lp16)
-        np.testing.assert_array_equal(d8.forward(9, n), d16.forward(9, n))  # the KV cache rows, bit for bit
+        for p8, p16 in zip(caches[0], caches[1]):  # every K / V cache row the prefill wrote, bit for bit
+            a, b = np.empty(kvb, np.uint8), np.empty(kvb, np.uint8)
+            R.check(R.lib.yalm_download(a.ctypes.data, p8, kvb))
+            R.check(R.lib.yalm_download(b.ctypes.data, p16, kvb))
+            np.testing.assert_array_equal(a, b)
         assert np.max(np.abs(lp8[: n - 1] - _decode_logprobs(dd, tokens))) <= LP_ATOL
     finally:
         for h in (d8, d16, dd, dm8, dm16):
             h.close()
+        for p in caches[0] + caches[1]:
+            R.lib.yalm_free(p)
 
 
 def test_prefill_range_guard_scales_glu_output():

@@ -238,7 +238,7 @@ def synth_seed(base: int, name: str) -> int:
     return h
 
 
-def synth_params(name: str, is_norm: bool, peak: float = 1.0, real: "Realistic" = None):
+def synth_params(name: str, is_norm: bool, peak: float = 1.0, real: "Realistic" = None, tied: bool = False):
     """(scale, offset) of a synthetic tensor. peak > 1 scales the final norm weight, so the
     logits spread peak x wider: the default model's logits have a std of ~1.2 (near-uniform
     next-token distributions). real: the realistic model's Wq / Wk gain and final-norm scale
@@ -249,9 +249,11 @@ def synth_params(name: str, is_norm: bool, peak: float = 1.0, real: "Realistic" 
         k = peak if name == "model.norm.weight" else 1.0
         return NORM_SCALE * k, NORM_OFFSET * k
     if real is not None and name.endswith((".attn.wq.weight", ".attn.wk.weight")):
-        return WEIGHT_SCALE * real.qk_gain, 0.0
+        return WEIGHT_SCALE * (real.qk_gain_tied if tied else real.qk_gain), 0.0
     if real is not None and name in ("model.embed.weight", "model.output.weight"):
-        return WEIGHT_SCALE * real.emb_gain, 0.0
+        return WEIGHT_SCALE * (real.emb_gain_tied if tied else real.emb_gain), 0.0
+    if real is not None and name.endswith((".attn.wo.weight", ".mlp.w2.weight")):
+        return WEIGHT_SCALE * real.branch_gain, 0.0
     return WEIGHT_SCALE, 0.0
 
 
@@ -271,12 +273,30 @@ PEAKED = 8.0  # synth_params(peak=PEAKED): the final norm x 8 (round 5; a pure l
 #     weight glu_value, so act(W1 x) * (W3 x) exceeds 65504 (the f16 range) at every position
 #     (reference infer.cpp:360-375 keeps it in f32); their W2 columns x w2_spike_cols;
 #   * a final-norm scale that is not a power of two (logits not an exact multiple of the
-#     uniform model's).
+#     uniform model's);
+#   * a residual stream that dominates its branches, as in trained models: the embedding and
+#     classifier x emb_gain, Wo and W2 x branch_gain. With full-size branches a random-weight
+#     model is chaotic (measured on the oracle, Mistral dims: a one-ulp change of ONE embedding
+#     element moves the logits by 1.6e-3 at 16 layers with the other features on, 2.9e-4 for
+#     the uniform model), so no two correct fp32 summation orders would agree to 1e-3 at 32
+#     layers; with these gains it moves them by 4.4e-5 at 32 layers.
+# Measured on the oracle (Mistral dims, 32 layers; Llama-3.2-3B dims, 28, tied): attention
+# top weight median 0.89 / 0.86 in the last layers, residual outliers ~100 / 64 / 258 against
+# other channels of std ~0.4 / 0.14, the layer-1 GLU product 1.6e5 / 8.4e4 at every position,
+# top-1 next-token probability median 0.54 (Mistral) / 0.997 (Llama: the tied classifier
+# favours the input token; log p of a uniformly random next token ~ -18).
 @dataclasses.dataclass(frozen=True)
 class Realistic:
-    qk_gain: float = 12.0
+    qk_gain: float = 24.0
     emb_gain: float = 16.0
-    final_norm: float = 0.7
+    # tied models (the classifier IS the embedding): a residual dominated by a x16 embedding
+    # makes the input token win by ~250 logits (measured, Llama dims); x4 leaves the layers'
+    # updates a share of it (top-1 gap ~15, an unlikely token's log p ~ -18, finite in the
+    # reference's f32 sample_prob), with the Wq / Wk gain raised to keep attention peaked
+    emb_gain_tied: float = 4.0
+    qk_gain_tied: float = 96.0
+    branch_gain: float = 0.125
+    final_norm: float = 4.5
     outliers: tuple = (96.0, -64.0, 256.0)
     outlier_norm: float = 1.0 / 64.0
     w2_outlier_gain: float = 8.0
@@ -393,7 +413,7 @@ def synth_host_tensors(c: ModelConfig, seed: int = 1, peak: float = 1.0, real: R
     c.weight_dtype storage: f32 / f16 / uint8 E5M2 bits); real: the realistic model."""
     out = {}
     for name, (shape, is_norm) in tensor_shapes(c).items():
-        scale, offset = synth_params(name, is_norm, peak, real)
+        scale, offset = synth_params(name, is_norm, peak, real, c.tied)
         dt = F32 if is_norm else c.weight_dtype
         n = int(np.prod(shape))
         out[name] = synth_array(n, dt, synth_seed(seed, name), scale, offset).reshape(shape)

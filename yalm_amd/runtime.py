@@ -351,7 +351,7 @@ class DeviceModel:
             dt = M.F32 if is_norm else cfg.weight_dtype
             eb = M.DTYPE_BYTES[dt]
             src_name = "model.embed.weight" if name == "tp.wcls" else name
-            scale, offset = M.synth_params(src_name, is_norm, peak, real)
+            scale, offset = M.synth_params(src_name, is_norm, peak, real, cfg.tied)
             sh = M.tp_shard(cfg, name, rank, size)
             if sh is None:
                 p = self._alloc(n * eb)
