@@ -316,6 +316,12 @@ def prefill_leg(runtime, M, model="llama-3.2-3b", n=4096, iters=3, check=48):
             lp_d.append(lg[tokens[pos + 1]] - m - np.log(np.exp(lg - m).sum()))
         seq_s = (time.perf_counter() - t0) / check
         err = float(np.max(np.abs(lp_p[:check] - np.array(lp_d))))
+        # the split-operand precision form (yalm_set_prefill_precision SPLIT: every activation
+        # operand as [hi | lo], what the CLI's -m perplexity runs), timed the same way
+        dec.set_prefill_precision(runtime.PREFILL_SPLIT)
+        ms_split = dec.prefill_time(n, max(1, iters - 1))
+        lp_s = dec.prefill(tokens)
+        err_split = float(np.max(np.abs(lp_s[:check] - np.array(lp_d))))
     finally:
         if dec2 is not None:
             dec2.close()
@@ -334,6 +340,11 @@ def prefill_leg(runtime, M, model="llama-3.2-3b", n=4096, iters=3, check=48):
         "sequential_decode_ms_per_position": round(seq_s * 1e3, 3),
         "speedup_vs_sequential": round(seq_s * n / (ms * 1e-3), 1),
         "spot_check": {"positions": check, "max_abs_dlogp_vs_decode": err},
+        "split_form": {"value": round(ms_split, 3), "unit": "ms",
+                       "what": "yalm_set_prefill_precision SPLIT (every f16 activation operand as [hi | lo]; "
+                               "-m perplexity's form), 2x the matrix work, same algorithmic flops counted",
+                       "tflops_algorithmic": round(flops / (ms_split * 1e-3) / 1e12, 1),
+                       "max_abs_dlogp_vs_decode": err_split},
         "data": "synthetic weights of the real Llama-3.2-3B shape, synthetic token ids",
     }
 

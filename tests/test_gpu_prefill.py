@@ -241,6 +241,7 @@ def test_bench_prefill_leg():
     assert rl["bound"] == "mfma" and 0 < rl["achieved"] and 0 < rl["frac"] < 1
     assert out["flops"] > 0 and out["tok_per_s"] > 0
     assert out["spot_check"]["max_abs_dlogp_vs_decode"] <= LP_ATOL
+    assert out["split_form"]["value"] > 0 and out["split_form"]["max_abs_dlogp_vs_decode"] <= LP_ATOL
 
 
 def _f16_twin(cfg8, t8):
