@@ -208,6 +208,18 @@ static void launch_v2(const uint16_t *Q, const uint16_t *kc, const uint16_t *vc,
 	                                                                                          nkv, O);
 }
 
+// the split-operand precision form (Q and O [hi | lo]; here Q's lo half reads the next row's
+// hi, O writes 2x wide: a timing of the doubled MFMA work, not a numerics check)
+static uint16_t *g_q2 = nullptr, *g_o2 = nullptr;
+static void launch_split(const uint16_t *Q, const uint16_t *kc, const uint16_t *vc, int T, int pos0, int nh, int nkv,
+						 uint16_t *O, hipStream_t st) {
+	const dim3 grid(nh, (T + pf::AQ - 1) / pf::AQ);
+	pf::attn_prefill_kernel<128, 64, true><<<grid, pf::THREADS, pf::attn_prefill_lds<128>(), st>>>(g_q2, kc, vc, T, pos0,
+	                                                                                              nh, nkv, g_o2);
+	(void)Q;
+	(void)O;
+}
+
 int main(int argc, char **argv) {
 	const int T = argc > 1 ? atoi(argv[1]) : 4096;
 	const int rounds = argc > 2 ? atoi(argv[2]) : 5;
@@ -236,7 +248,12 @@ int main(int argc, char **argv) {
 	                       (int)pf::attn_prefill_lds<128>()));
 	CK(hipFuncSetAttribute((const void *)pf::attn_prefill_kernel<128, 32>, hipFuncAttributeMaxDynamicSharedMemorySize,
 	                       (int)pf::attn_prefill_lds<128, 32>()));
-	std::vector<Variant> vs = {{"r3", launch_v0}, {"product", launch_v1}, {"kt32", launch_v2}};
+	CK(hipFuncSetAttribute((const void *)pf::attn_prefill_kernel<128, 64, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+	                       (int)pf::attn_prefill_lds<128>()));
+	CK(hipMalloc(&g_q2, 2 * qn * 2));
+	CK(hipMalloc(&g_o2, 2 * qn * 2));
+	CK(hipMemset(g_q2, 0, 2 * qn * 2));
+	std::vector<Variant> vs = {{"product", launch_v1}, {"r3", launch_v0}, {"split", launch_split}};
 	const int nv = (int)vs.size();
 	std::vector<uint16_t *> outs(nv);
 	for (auto &o : outs)
