@@ -80,8 +80,8 @@ class Pair:
             rt().lib.yalm_free(p)
 
 
-@pytest.fixture(scope="module", params=[(M.F16, None), (M.F8E5M2, None), (M.F16, M.REALISTIC)],
-                ids=["f16", "fp8", "f16-realistic"])
+@pytest.fixture(scope="module", params=[(M.F16, None), (M.F8E5M2, None), (M.F16, M.REALISTIC), (M.F8E5M2, M.REALISTIC)],
+                ids=["f16", "fp8", "f16-realistic", "fp8-realistic"])
 def model(request):
     """realistic: models.REALISTIC -- peaked attention, residual outlier
     channels of 10^2..10^3, a GLU product above 65504 in layer 1 (f32 on both sides in the

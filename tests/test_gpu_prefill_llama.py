@@ -70,12 +70,14 @@ def test_prefill_llama3b_dims_vs_oracle():
     assert d_max <= LP_MAX, d_max
 
 
+@pytest.mark.parametrize("form", ["fast", "split"])
 @pytest.mark.parametrize("depth", [14, 28])
-def test_prefill_llama3b_full_depth_vs_oracle(depth):
+def test_prefill_llama3b_full_depth_vs_oracle(depth, form):
     """The real depth (28 layers; 14 as the midpoint of the depth curve) at the real
     dims over 256 positions in one prefill pass, against the oracle's sequential
     perplexity loop (main.cpp:174-184): the f16 activation rounding compounds with
-    depth, so the bars are checked where it is largest."""
+    depth, so the bars are checked where it is largest; in both prefill forms (the
+    split-operand form, -m perplexity's, carries the activations to ~2^-22)."""
     cfg = M.LLAMA_32_3B.with_(n_layers=depth, max_seq_len=256)
     n = 256
     tokens = np.random.default_rng(1000 + depth).integers(0, cfg.vocab_size, size=n).astype(np.int32)
@@ -83,6 +85,8 @@ def test_prefill_llama3b_full_depth_vs_oracle(depth):
     dm = R.DeviceModel.synthetic(cfg, seed=6)
     dec = R.Decoder(dm)
     try:
+        if form == "split":
+            dec.set_prefill_precision(R.PREFILL_SPLIT)
         lp = dec.prefill(tokens)[: n - 1].astype(np.float64)
     finally:
         dec.close()
@@ -92,7 +96,7 @@ def test_prefill_llama3b_full_depth_vs_oracle(depth):
     lo = oracle_logprobs(om, tokens)
     d = np.abs(lp - lo)
     d_ppl = abs(lp.mean() - lo.mean())
-    print(f"llama-3b dims, {depth} layers, {n} positions: |d log ppl| {d_ppl:.2e}, max |d log p| {d.max():.2e}, "
+    print(f"llama-3b dims, {depth} layers, {form} form, {n} positions: |d log ppl| {d_ppl:.2e}, max |d log p| {d.max():.2e}, "
           f"p99 {np.quantile(d, 0.99):.2e}, median {np.median(d):.2e}, log ppl {-lo.mean():.4f}")
     assert np.all(np.isfinite(lp))
     assert d_ppl <= LOGPPL_TOL, d_ppl
