@@ -398,28 +398,34 @@ int ensure_bufs(yalm_decoder_s *d) {
 	return YALM_OK;
 }
 
-template <int ACT>
-int enqueue_glu(yalm_decoder_s *d, const yalm_block_weights &w, int T, float hscale, unsigned *range) {
+template <int ACT, bool SPLIT>
+int enqueue_glu_t(yalm_decoder_s *d, const yalm_block_weights &w, int T, float hscale, unsigned *range) {
 	const yalm_config &c = d->c;
 	const PfForms &f = d->pf_forms;
 	const int bn = pick_bn(f, PG_GLU, T, 2 * c.hidden_dim, true);
-	const int sp = f.split ? 2 : 1; // split-operand form: A = [hi | lo] (K = 2 dim), H rows [hi | lo]
-	pf::E16Glu<ACT> e;
+	const int sp = SPLIT ? 2 : 1; // split-operand form: A = [hi | lo] (K = 2 dim), H rows [hi | lo]
+	pf::E16Glu<ACT, SPLIT> e;
 	e.h = d->pf.H;
 	e.ldh = c.hidden_dim * sp;
 	e.M = T;
 	e.hscale = hscale;
 	e.range = range;
-	e.lo_off = f.split ? c.hidden_dim : 0;
+	e.lo_off = SPLIT ? c.hidden_dim : 0;
 	pf::BRowsGlu<64> bm{(const uint16_t *)w.w1, (const uint16_t *)w.w3};
 	if (bn == 256)
-		return launch_g16_t<pf::E16Glu<ACT>, pf::BRowsGlu<64>, 256, 2>(f, d->pf.Xn, sp * c.dim, T, sp * c.dim, c.dim,
+		return launch_g16_t<pf::E16Glu<ACT, SPLIT>, pf::BRowsGlu<64>, 256, 2>(f, d->pf.Xn, sp * c.dim, T, sp * c.dim, c.dim,
                                                                      bm, 2 * c.hidden_dim, e, d->stream);
 	if (bn == 128)
-		return launch_g16_t<pf::E16Glu<ACT>, pf::BRowsGlu<64>, 128, 4>(f, d->pf.Xn, sp * c.dim, T, sp * c.dim, c.dim,
+		return launch_g16_t<pf::E16Glu<ACT, SPLIT>, pf::BRowsGlu<64>, 128, 4>(f, d->pf.Xn, sp * c.dim, T, sp * c.dim, c.dim,
                                                                      bm, 2 * c.hidden_dim, e, d->stream);
 	set_err("prefill GLU GEMM: 2 x hidden_dim must divide by 128 (or by a forced width of 128 / 256)");
 	return YALM_ERR_UNSUPPORTED;
+}
+
+template <int ACT>
+int enqueue_glu(yalm_decoder_s *d, const yalm_block_weights &w, int T, float hscale, unsigned *range) {
+	return d->pf_forms.split ? enqueue_glu_t<ACT, true>(d, w, T, hscale, range)
+	                         : enqueue_glu_t<ACT, false>(d, w, T, hscale, range);
 }
 
 // The whole prefill on d->stream: T rows at positions pos0 .. pos0 + T - 1. hexp[l] (null:
@@ -496,8 +502,7 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp, const int 
 			e.head_dim = c.head_dim;
 			e.pos0 = pos0;
 			e.clip = c.qkv_clip;
-				e.range = rg + RG_Q;
-				e.q_lo = split ? q_dim : 0;
+			e.range = rg + RG_Q;
 			// QKV + clip + RoPE as two GEMMs: q (K = dim over hi) and k | v from column
 			// q_dim (K = 2 dim over hi | lo, the B rows wrapping at dim)
 			if (small) {
@@ -508,8 +513,12 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp, const int 
 				                  st));
 				TRY(launch_skinny_reduce<false>(b.skp, ks_qkv, 2 * ks_qkv, q_dim, T, np, e, st));
 			} else {
-				if (split) { // q | k | v all over [hi | lo]
-					TRY(launch_plain(f, bn_qkv_all, b.Xn, 2 * c.dim, T, 2 * c.dim, c.dim, qkv, q_dim + 2 * kv_dim, e, st));
+				if (split) { // q | k | v all over [hi | lo], Q stored [hi | lo]
+					pf::E16QKVt<true> es;
+					es.q = e.q, es.kc = e.kc, es.vc = e.vc, es.rope = e.rope, es.M = e.M, es.q_dim = e.q_dim;
+					es.kv_dim = e.kv_dim, es.head_dim = e.head_dim, es.pos0 = e.pos0, es.clip = e.clip;
+					es.range = e.range, es.q_lo = q_dim;
+					TRY(launch_plain(f, bn_qkv_all, b.Xn, 2 * c.dim, T, 2 * c.dim, c.dim, qkv, q_dim + 2 * kv_dim, es, st));
 				} else if (qkv1) { // one launch: the k | v tiles (K = 2 dim) first, then the q tiles (K = dim)
 					TRY((launch_g8p<pf::E16QKV, pf::BRowsPlain, 2, 2>(f, b.Xn, 2 * c.dim, T, c.dim, c.dim,
 					                                                   pf::BRowsPlain{qkv}, q_dim + 2 * kv_dim, e, st,

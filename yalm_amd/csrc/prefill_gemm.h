@@ -150,7 +150,11 @@ __device__ __forceinline__ float act_fast(float x) {
 // layer's GLU products exceed the f16 range (prefill.hip: found by range_note, the pass
 // re-run with the scale, the W2 epilogue multiplying by 2^e); values below 2^-14 * 2^e then
 // lose relative precision as f16 subnormals, far under the W2 sum's own rounding.
-template <int ACT>
+// The range check is one v_max with an |abs| modifier per element: finite operands give a
+// finite or overflowing (inf, caught) product, and a NaN needs an inf or NaN upstream,
+// which the row norms' checks catch. SPLIT (the split-operand form): H rows [hi | lo], lo
+// `hidden` columns after hi (ldh = 2 hidden).
+template <int ACT, bool SPLIT = false>
 struct E16Glu {
 	static constexpr bool NEEDS_LDS = false;
 	float *red = nullptr;
@@ -158,7 +162,7 @@ struct E16Glu {
 	int ldh, M;
 	float hscale = 1.0f;
 	unsigned *range = nullptr;
-	int lo_off = 0; // split-operand form: f16(v - hi) stored lo_off columns after hi (H rows [hi | lo])
+	int lo_off = 0; // SPLIT: columns from hi to lo
 	template <int FI, int FJ>
 	__device__ __forceinline__ void apply(f32x4_t (&acc)[FI][FJ], int m0, int n0, int lane, int, int) const {
 		float vmax = 0.0f;
@@ -172,12 +176,12 @@ struct E16Glu {
 #pragma unroll
 				for (int j = 0; j < FJ / 2; ++j) {
 					const float v = act_fast<ACT>(acc[i][j][r]) * acc[i][j + FJ / 2][r];
-					vmax = fmaxf(vmax, v != v ? __builtin_inff() : fabsf(v)); // NaN counts as inf
+					vmax = fmaxf(vmax, fabsf(v));
 					const float vs = v * hscale;
 					const uint16_t hb = f2h_bits(vs);
 					uint16_t *const hp = h + (size_t)m * ldh + n0 + 16 * j + (lane & 15);
 					hp[0] = hb;
-					if (lo_off)
+					if constexpr (SPLIT)
 						hp[lo_off] = f2h_bits(vs - h2f(hb));
 				}
 			}
@@ -193,7 +197,9 @@ struct E16Glu {
 // lane are loaded unconditionally (rows clamped) before any use: with per-element
 // region / row branches hipcc waited for each table load separately (the epilogue cost
 // 71 of 172 us at Llama-3B T 4096, tools/gemm_epi_bench.hip).
-struct E16QKV {
+// SPLITQ (the split-operand form): Q rows [hi | lo], lo q_lo (= q_dim) columns after hi.
+template <bool SPLITQ = false>
+struct E16QKVt {
 	static constexpr bool NEEDS_LDS = false;
 	float *red = nullptr;
 	uint16_t *q;
@@ -201,9 +207,10 @@ struct E16QKV {
 	const float *rope;
 	int M, q_dim, kv_dim, head_dim, pos0;
 	float clip;
-	unsigned *range = nullptr; // the f16 Q operand out of range (range_note); K / V are the
-							   // f16 cache rows of the reference too (infer.cpp:299)
-	int q_lo = 0;              // split-operand form: Q rows [hi | lo], lo q_lo columns after hi
+	unsigned *range = nullptr; // the f16 Q operand out of range (range_note, |max| only: see
+							   // E16Glu); K / V are the f16 cache rows of the reference too
+							   // (infer.cpp:299)
+	int q_lo = 0;
 	template <int FI, int FJ>
 	__device__ __forceinline__ void apply(f32x4_t (&acc)[FI][FJ], int m0, int n0, int lane, int, int) const {
 		const bool odd = lane & 1;
@@ -217,7 +224,7 @@ struct E16QKV {
 			const int fj = (nn % head_dim) >> 1;
 			const bool rot = region != 2;
 			uint16_t *const dst = (region == 0 ? q : (region == 1 ? kc : vc)) + nn;
-			const int ld = region == 0 ? q_dim + q_lo : kv_dim, roff = region == 0 ? 0 : pos0;
+			const int ld = region == 0 ? (SPLITQ ? 2 * q_dim : q_dim) : kv_dim, roff = region == 0 ? 0 : pos0;
 			constexpr int IB = FI < 4 ? FI : 4; // row fragments per batch of table loads
 #pragma unroll
 			for (int i0 = 0; i0 < FI; i0 += IB) {
@@ -239,13 +246,14 @@ struct E16QKV {
 						const float ro = odd ? p * cs[i][r][1] + v * cs[i][r][0] : v * cs[i][r][0] - p * cs[i][r][1];
 						const int m = m0 + 16 * (i0 + i) + crow16(r, lane);
 						const float o = rot ? ro : v;
-						if (region == 0 && m < M)
-							qmax = fmaxf(qmax, o != o ? __builtin_inff() : fabsf(o));
 						if (m < M) {
 							const uint16_t ob = f2h(o);
 							dst[(size_t)(roff + m) * ld] = ob;
-							if (region == 0 && q_lo)
-								dst[(size_t)m * ld + q_lo] = f2h(o - h2f(ob));
+							if (region == 0) {
+								qmax = fmaxf(qmax, fabsf(o));
+								if constexpr (SPLITQ)
+									dst[(size_t)m * ld + q_lo] = f2h(o - h2f(ob));
+							}
 						}
 					}
 			}
@@ -253,6 +261,7 @@ struct E16QKV {
 		range_note(range, qmax, qmax);
 	}
 };
+using E16QKV = E16QKVt<false>;
 
 // Per (row, BN-column tile): max and sum of exp over the tile's logits, and the
 // target token's logit when it falls in the tile (sample_prob, sampler.cpp:11-25,
