@@ -199,9 +199,11 @@ int yalm_attn_wo_plan(const yalm_config *config, int slots, int *splits, int *gr
  * YALM_ATTN_WO_TRACE=1): 16 stamps per workgroup at [w * 16 + k]: k < 8
  * s_memrealtime (100 MHz), k + 8 the shader clock (s_memtime) at the same point; k = 0 start, 1 hand-off signalled (attention; 0 if this workgroup did not
  * finish a kv head) or Wo slice landed (Wo; the trace waits for it), 2 poll passed (Wo) or
- * first K/V/q loads landed (attention; the trace waits for them), 3 end; attention only:
- * 4 scores in LDS, 5 softmax done, 6 P.V partials in LDS, 7 merger's gather done. Workgroups
- * [0, *attention_workgroups) are attention, the rest Wo. */
+ * first K/V/q loads landed (attention; the trace waits for them), 3 end; attention units:
+ * 4 scores of the last chunk, 5 its softmax, 6 P.V sums combined, 7 head outputs / partials
+ * issued; merger workgroups (2 and 4 read 0): 5 gather issued, 7 every partial seen. A
+ * phase a workgroup never reached reads 0. Workgroups [0, *attention_workgroups) are
+ * attention units and mergers, the rest Wo. */
 int yalm_attn_wo_trace(yalm_decoder d, unsigned long long *host, size_t count, int *workgroups,
                        int *attention_workgroups);
 

@@ -55,20 +55,41 @@ def main():
           f"launch span {us[:, 3].max():.2f} us")
     print(f"attention start  {q(att[:, 0])}")
     print(f"attention end    {q(att[:, 3])}")
-    active = att[tr[:na, 2] > 0]
-    print(f"active attention workgroups: {len(active)}")
+    # attention units stamp [2] (first loads landed); mergers leave it 0 and stamp [5] / [7]
+    # (gather issued / every partial seen); a phase a workgroup never reached reads 0
+    act_m = tr[:na, 2] > 0
+    mer_m = (tr[:na, 2] == 0) & (tr[:na, 7] > 0)
+    active = att[act_m]
+    print(f"active attention units: {len(active)}")
     print(f"  loads landed   {q(active[:, 2])}")
-    print(f"  scores in LDS  {q(active[:, 4])}")
-    print(f"  softmax done   {q(active[:, 5])}")
-    print(f"  P.V in LDS     {q(active[:, 6])}")
-    a_tr, a_clk = tr[:na][tr[:na, 2] > 0], clk[:na][tr[:na, 2] > 0]
-    for k0, k1, name in ((2, 4, "loads->scores"), (4, 5, "scores->softmax"), (5, 6, "softmax->P.V"), (6, 1, "P.V->signal")):
-        dt = (a_tr[:, k1] - a_tr[:, k0]) / 100.0
-        dc = a_clk[:, k1] - a_clk[:, k0]
-        print(f"  {name:16s} {np.median(dt):6.2f} us  {np.median(dc):8.0f} shader clocks  ({np.median(dc) / np.maximum(np.median(dt), 1e-3) / 1e3:5.2f} GHz)")
-    mergers = att[tr[:na, 7] > 0]
-    if len(mergers):
-        print(f"  merger gathered {q(mergers[:, 7])}  ({len(mergers)} mergers)")
+    print(f"  last scores    {q(active[:, 4])}")
+    print(f"  last softmax   {q(active[:, 5])}")
+    print(f"  P.V combined   {q(active[:, 6])}")
+    print(f"  outputs issued {q(active[:, 7])}")
+    a_tr, a_clk = tr[:na][act_m], clk[:na][act_m]
+
+    def phase(rows, rclk, k0, k1, name):
+        dt = (rows[:, k1] - rows[:, k0]) / 100.0
+        dc = rclk[:, k1] - rclk[:, k0]
+        print(f"  {name:18s} med {np.median(dt):6.2f} max {dt.max():6.2f} us  {np.median(dc):8.0f} shader clocks"
+              f"  ({np.median(dc) / np.maximum(np.median(dt), 1e-3) / 1e3:5.2f} GHz)")
+
+    for k0, k1, name in ((0, 2, "start->loads"), (2, 4, "loads->last scores"), (4, 5, "scores->softmax"),
+                         (5, 6, "softmax->P.V"), (6, 7, "P.V->issued")):
+        phase(a_tr, a_clk, k0, k1, name)
+    if mer_m.any():
+        m_tr, m_clk = tr[:na][mer_m], clk[:na][mer_m]
+        mergers = att[mer_m]
+        print(f"mergers: {len(mergers)}")
+        print(f"  gather issued  {q(mergers[:, 5])}")
+        print(f"  all partials   {q(mergers[:, 7])}")
+        print(f"  head signalled {q(mergers[:, 1])}")
+        # the hop: the last partial of this merger's head issued -> seen -> head out
+        phase(m_tr, m_clk, 5, 7, "spin (issued->seen)")
+        phase(m_tr, m_clk, 7, 1, "fold->signalled")
+        last_part = active[:, 7].max()
+        print(f"  last partial issued {last_part:6.2f} us; last partial seen {mergers[:, 7].max():6.2f} us; "
+              f"last head {mergers[:, 1].max():6.2f} us")
     print(f"head signalled   {q(writers[:, 1])}  ({len(writers)} writers)")
     print(f"Wo start         {q(wo[:, 0])}")
     print(f"Wo slice landed  {q(wo[:, 1])}")

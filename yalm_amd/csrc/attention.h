@@ -598,6 +598,7 @@ __device__ __forceinline__ bool attn_core(int g, int hq0, int Gh, int c_first, i
 			}
 		}
 	}
+	stamp(7); // this workgroup's head outputs / partials issued
 	if (final_out && att_dbg) { // test hook: raw scores -> probabilities
 		const int nt = kv_len;
 		for (int i = tid; i < Gh * nt; i += ATTN_THREADS) {
@@ -704,7 +705,8 @@ template <int D, bool GRAN>
 __device__ __forceinline__ bool attn_merge_body(int g, int hq, int S, int head_max, const StepState *step, int n_heads,
                                                 int n_kv_heads, int max_seq_len, int nsplit,
                                                 const unsigned long long *part, unsigned ptag, unsigned *err,
-                                                float *out, float *att_dbg, unsigned gtag = 0) {
+                                                float *out, float *att_dbg, unsigned gtag = 0,
+                                                unsigned long long *ts = nullptr) {
 	constexpr int CHUNK = attn_chunk<D>();
 	constexpr int SPW = ATTN_MAX_SPLITS / ATTN_WAVES; // splits per wave, at most
 	constexpr int E = D >= 64 ? D / 64 : 1;           // dims per lane: lane + 64 k
@@ -723,6 +725,8 @@ __device__ __forceinline__ bool attn_merge_body(int g, int hq, int S, int head_m
 	const unsigned long long *ph = part + (size_t)h * nsplit * (D + 2);
 	const unsigned long long *pl = ph + (size_t)(wave + ATTN_WAVES * min(lane, max(nsw - 1, 0))) * (D + 2);
 	const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + ATTN_TIMEOUT;
+	if (ts) // trace (attn_wo.h, thread 0): [5] gather issued, [7] every partial seen (merger rows keep [2] = 0)
+		ts[5] = __builtin_amdgcn_s_memrealtime(), ts[13] = __builtin_amdgcn_s_memtime();
 	bool alive = true;
 	float ms = -FLT_MAX, ls = 0.0f, ob[SPW][E];
 	for (;;) {
@@ -769,6 +773,8 @@ __device__ __forceinline__ bool attn_merge_body(int g, int hq, int S, int head_m
 	if (lane == 0)
 		mml[wave][0] = mw;
 	__syncthreads();
+	if (ts) // every wave's partials in registers
+		ts[7] = __builtin_amdgcn_s_memrealtime(), ts[15] = __builtin_amdgcn_s_memtime();
 	const float M = fmaxf(fmaxf(mml[0][0], mml[1][0]), fmaxf(mml[2][0], mml[3][0]));
 	const float ws = lane < nsw ? expf(ms - M) : 0.0f;
 	const float lw = wave_sum(ws * ls);

@@ -211,13 +211,18 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 	const unsigned epoch = step->epoch; // this launch's tag (step_begin_kernel / set_step_full_kernel)
 	if (b < munits) { // ---- attention or merger workgroup
 		const unsigned ptag = epoch * (unsigned)p.n_layers + (unsigned)p.layer;
+		if (tr) { // phases this workgroup never reaches read 0, not an earlier launch's stamps
+			tr[2] = tr[10] = 0;
+			for (int k = 4; k < 8; ++k)
+				tr[k] = tr[8 + k] = 0;
+		}
 		const bool wrote =
 		    b < units ? attn_decode_body<D, GT, true>(b % p.n_kv, b / p.n_kv, p.S, p.head_max, q, kc, vc, step,
 		                                               p.n_heads, p.n_kv, p.max_seq_len, p.nsplit, p.part, ptag,
 		                                               (float *)p.gran, nullptr, epoch, tr, p.trace != nullptr)
 		              : attn_merge_body<D, true>((b - units) % p.n_kv, (b - units) / p.n_kv, p.S, p.head_max, step,
 		                                         p.n_heads, p.n_kv, p.max_seq_len, p.nsplit, p.part, ptag, p.err,
-		                                         (float *)p.gran, nullptr, epoch);
+		                                         (float *)p.gran, nullptr, epoch, tr);
 		if (tr) { // the head outputs are their own ready flags: nothing to drain or signal
 			const unsigned long long t1 = __builtin_amdgcn_s_memrealtime(), c1 = __builtin_amdgcn_s_memtime();
 			tr[0] = t_start, tr[8] = c_start;
