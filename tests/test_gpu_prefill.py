@@ -54,7 +54,8 @@ FORMS = {"auto": "", "auto-qkv2": "qkv1:0",
          "g16-192-2ph": G16_ALL.format(192) + ",8p:0",
          "g16-128-2ph": G16_ALL.format(128) + ",8p:0",
          "g16-256-nopersist": G16_ALL.format(256) + ",persist:0",
-         "g16-320": G16_ALL.format(320)}
+         "g16-320": G16_ALL.format(320),
+         "wnorm0": "wnorm:0"}  # the workgroup-per-row norm kernel (round 6 default: one wave per row)
 
 
 @pytest.mark.parametrize("form", list(FORMS))

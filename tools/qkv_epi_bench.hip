@@ -39,10 +39,11 @@ __device__ __forceinline__ void quad_transpose(float (&v)[4], int lane) {
 	}
 }
 
-// MODE 0 prod, 1 notab, 2 nostore, 3 tr4
+// MODE 0 prod, 1 notab, 2 nostore, 3 tr4, 4 the tile's RoPE rows staged in LDS (one
+// contiguous 128-KB copy: rows m0t .. m0t + 255 x 64 (cos, sin)), 5 = 4 + tr4
 template <int MODE>
 struct E16QKVd {
-	static constexpr bool NEEDS_LDS = false;
+	static constexpr bool NEEDS_LDS = MODE >= 4;
 	float *red = nullptr;
 	uint16_t *q;
 	uint16_t *kc, *vc;
@@ -52,6 +53,16 @@ struct E16QKVd {
 	template <int FI, int FJ>
 	__device__ __forceinline__ void apply(f32x4_t (&acc)[FI][FJ], int m0, int n0, int lane, int, int) const {
 		const bool odd = lane & 1;
+		const int m0t = m0 - (m0 % G_BM); // the tile's first row
+		if constexpr (MODE >= 4) { // rows m0t .. m0t + 255 of the table: 128 KB, contiguous
+			const float4_t *src = (const float4_t *)(rope + (size_t)m0t * (head_dim >> 1) * 2);
+			float4_t *dst = (float4_t *)red;
+			const int nrow = min(G_BM, M - m0t);
+			const int n16 = nrow * (head_dim >> 1) * 2 / 4;
+			for (int i = threadIdx.x; i < n16; i += G_THREADS)
+				dst[i] = src[i];
+			__syncthreads();
+		}
 #pragma unroll
 		for (int j = 0; j < FJ; ++j) {
 			const int nb = __builtin_amdgcn_readfirstlane(n0 + 16 * j);
@@ -72,6 +83,9 @@ struct E16QKVd {
 					for (int r = 0; r < 4; ++r) {
 						if constexpr (MODE == 1) {
 							cs[i][r] = float2_t{c0, s0};
+						} else if constexpr (MODE >= 4) {
+							const int ml = min(m0 + 16 * (i0 + i) + crow16(r, lane), M - 1) - m0t;
+							cs[i][r] = *(const float2_t *)(red + ((size_t)ml * (head_dim >> 1) + fj) * 2);
 						} else {
 							const int m = min(m0 + 16 * (i0 + i) + crow16(r, lane), M - 1);
 							cs[i][r] = *(const float2_t *)(rope + ((size_t)m * (head_dim >> 1) + fj) * 2);
@@ -89,7 +103,7 @@ struct E16QKVd {
 						ov[r] = rot ? ro : v;
 					}
 					const int mb = m0 + 16 * (i0 + i);
-					if constexpr (MODE == 3) {
+					if constexpr (MODE == 3 || MODE == 5) {
 						float hv[4];
 #pragma unroll
 						for (int r = 0; r < 4; ++r)
@@ -250,17 +264,19 @@ int main() {
 		e.pos0 = 0, e.clip = 3.4e38f;
 		return e;
 	};
-	const auto e0 = qkv(pf::E16QKVd<0>{}, Q, KC, VC);
-	const auto e1 = qkv(pf::E16QKVd<1>{}, Q, KC, VC);
-	const auto e2 = qkv(pf::E16QKVd<2>{}, Q, KC, VC);
-	const auto e3 = qkv(pf::E16QKVd<3>{}, Q2, KC2, VC2);
+	auto e0 = qkv(pf::E16QKVd<0>{}, Q, KC, VC);
+	auto e1 = qkv(pf::E16QKVd<1>{}, Q, KC, VC);
+	auto e2 = qkv(pf::E16QKVd<2>{}, Q, KC, VC);
+	auto e3 = qkv(pf::E16QKVd<3>{}, Q2, KC2, VC2);
+	auto e4 = qkv(pf::E16QKVd<4>{}, Q2, KC2, VC2);
+	auto e5 = qkv(pf::E16QKVd<5>{}, Q2, KC2, VC2);
 	pf::E16GluD<0> g0;
 	g0.h = H, g0.ldh = 8192, g0.M = M;
 	pf::E16GluD<2> g2;
 	g2.h = H, g2.ldh = 8192, g2.M = M;
 	pf::E16GluD<3> g3;
 	g3.h = H2, g3.ldh = 8192, g3.M = M;
-	const int NV = 10;
+	const int NV = 14;
 	std::vector<float> t[NV];
 	for (int r = 0; r < 7; ++r) {
 		t[0].push_back(run<decltype(e0), pf::BRowsPlain, 2, 2>(A, M, 3072, bp, 5120, e0, 10));
@@ -273,9 +289,14 @@ int main() {
 		t[7].push_back(run<pf::E16GluD<0>, pf::BRowsGlu<64>, 2, 2>(A, M, 3072, bg, 16384, g0, 10));
 		t[8].push_back(run<pf::E16GluD<2>, pf::BRowsGlu<64>, 2, 2>(A, M, 3072, bg, 16384, g2, 10));
 		t[9].push_back(run<pf::E16GluD<3>, pf::BRowsGlu<64>, 2, 2>(A, M, 3072, bg, 16384, g3, 10));
+		t[10].push_back(run<decltype(e4), pf::BRowsPlain, 2, 2>(A, M, 3072, bp, 5120, e4, 10));
+		t[11].push_back(run<decltype(e5), pf::BRowsPlain, 2, 2>(A, M, 3072, bp, 5120, e5, 10));
+		t[12].push_back(run320<decltype(e4)>(A, M, 3072, bp, 5120, e4, 10));
+		t[13].push_back(run320<decltype(e5)>(A, M, 3072, bp, 5120, e5, 10));
 	}
 	const char *nm[NV] = {"QKV 8p prod", "QKV 8p notab", "QKV 8p nostore", "QKV 8p tr4", "QKV 320 prod",
-	                      "QKV 320 tr4", "QKV 320 nostore", "GLU 8p prod", "GLU 8p nostore", "GLU 8p tr4"};
+	                      "QKV 320 tr4", "QKV 320 nostore", "GLU 8p prod", "GLU 8p nostore", "GLU 8p tr4",
+	                      "QKV 8p ldstab", "QKV 8p ldstab+tr4", "QKV 320 ldstab", "QKV 320 ldstab+tr4"};
 	for (int i = 0; i < NV; ++i) {
 		std::sort(t[i].begin(), t[i].end());
 		printf("%-18s median %7.1f us  min %7.1f us\n", nm[i], t[i][t[i].size() / 2], t[i][0]);
@@ -292,6 +313,17 @@ int main() {
 	};
 	run<decltype(e0), pf::BRowsPlain, 2, 2>(A, M, 3072, bp, 5120, e0, 1);
 	run<decltype(e3), pf::BRowsPlain, 2, 2>(A, M, 3072, bp, 5120, e3, 1);
+	printf("tr4 vs prod mismatches (8p): Q %zu K %zu V %zu\n", same(Q, Q2, (size_t)M * 3072),
+	       same(KC, KC2, (size_t)M * 1024), same(VC, VC2, (size_t)M * 1024));
+	run<decltype(e5), pf::BRowsPlain, 2, 2>(A, M, 3072, bp, 5120, e5, 1);
+	hipDeviceSynchronize();
+	printf("ldstab+tr4 vs prod mismatches (8p): Q %zu K %zu V %zu\n", same(Q, Q2, (size_t)M * 3072),
+	       same(KC, KC2, (size_t)M * 1024), same(VC, VC2, (size_t)M * 1024));
+	run320<decltype(e0)>(A, M, 3072, bp, 5120, e0, 1);
+	run320<decltype(e4)>(A, M, 3072, bp, 5120, e4, 1);
+	hipDeviceSynchronize();
+	printf("ldstab vs prod mismatches (320): Q %zu K %zu V %zu\n", same(Q, Q2, (size_t)M * 3072),
+	       same(KC, KC2, (size_t)M * 1024), same(VC, VC2, (size_t)M * 1024));
 	run<pf::E16GluD<0>, pf::BRowsGlu<64>, 2, 2>(A, M, 3072, bg, 16384, g0, 1);
 	run<pf::E16GluD<3>, pf::BRowsGlu<64>, 2, 2>(A, M, 3072, bg, 16384, g3, 1);
 	hipDeviceSynchronize();

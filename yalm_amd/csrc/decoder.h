@@ -95,6 +95,7 @@ struct PfForms {
 	bool skl = true;        // skinny GEMMs: weight rows staged by LDS-DMA (prefill_skinny.h)
 	bool split = false;     // split-operand precision form (yalm_set_prefill_precision): every f16
 							// activation operand as [hi | lo], the large-tile GEMMs at every T
+	bool wnorm = true;      // row norms: one wave per row, the row in registers (rmsnorm_rows_wave_kernel)
 };
 PfForms pf_forms_default(); // prefill.hip: the production forms (A/B build: YALM_PF_FORMS)
 

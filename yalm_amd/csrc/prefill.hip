@@ -25,7 +25,8 @@
 // explicitly through yalm_set_prefill_forms: "qkv:256,wo:128,..." forces widths, 8p:0
 // the 2-phase kernel, persist:0 one workgroup per tile, skinny:0 the large tiles at
 // T <= 64 too (prefill_skinny.h otherwise), qkv1:0 the q and k | v GEMMs as two
-// launches, skl:0 the skinny GEMMs' weights as register loads instead of LDS-DMA stages.
+// launches, skl:0 the skinny GEMMs' weights as register loads instead of LDS-DMA stages,
+// wnorm:0 the workgroup-per-row norm kernel instead of one wave per row.
 // The production library reads no environment for them; the A/B build (-DYALM_AB)
 // takes a decoder's initial forms from YALM_PF_FORMS (same syntax).
 static int parse_pf_forms(const char *spec, PfForms &f) {
@@ -61,6 +62,8 @@ static int parse_pf_forms(const char *spec, PfForms &f) {
 			f.skl = val != 0, known = true;
 		else if (!strcmp(key, "split"))
 			f.split = val != 0, known = true;
+		else if (!strcmp(key, "wnorm"))
+			f.wnorm = val != 0, known = true;
 		if (!known) {
 			set_err(std::string("yalm_set_prefill_forms: unknown key '") + key + "'");
 			return YALM_ERR_ARG;
@@ -312,6 +315,39 @@ int dequant(yalm_decoder_s *d, std::initializer_list<std::pair<const void *, siz
 	return YALM_OK;
 }
 
+// Xn = f16(rmsnorm(X) * w) rows (SPLIT: [hi | lo]): one wave per row with the row in
+// registers (prefill.h rmsnorm_rows_wave_kernel) when dim <= 8192, else (or forms "wnorm:0")
+// the workgroup-per-row kernel
+template <bool SPLIT>
+int launch_rmsnorm_t(const PfForms &f, const float *X, const float *w, int dim, int T, float eps, uint16_t *Xn,
+                     unsigned *range, hipStream_t st) {
+	const int nv = (dim / 4 + 63) / 64; // float4 per lane
+	const int g = (T + 3) / 4;
+	if (f.wnorm && nv <= 32) {
+		if (nv <= 4)
+			pf::rmsnorm_rows_wave_kernel<SPLIT, 4><<<g, 256, 0, st>>>(X, w, dim, T, eps, Xn, range);
+		else if (nv <= 8)
+			pf::rmsnorm_rows_wave_kernel<SPLIT, 8><<<g, 256, 0, st>>>(X, w, dim, T, eps, Xn, range);
+		else if (nv <= 12)
+			pf::rmsnorm_rows_wave_kernel<SPLIT, 12><<<g, 256, 0, st>>>(X, w, dim, T, eps, Xn, range);
+		else if (nv <= 16)
+			pf::rmsnorm_rows_wave_kernel<SPLIT, 16><<<g, 256, 0, st>>>(X, w, dim, T, eps, Xn, range);
+		else if (nv <= 24)
+			pf::rmsnorm_rows_wave_kernel<SPLIT, 24><<<g, 256, 0, st>>>(X, w, dim, T, eps, Xn, range);
+		else
+			pf::rmsnorm_rows_wave_kernel<SPLIT, 32><<<g, 256, 0, st>>>(X, w, dim, T, eps, Xn, range);
+	} else {
+		pf::rmsnorm_rows_kernel<SPLIT><<<T, 256, 0, st>>>(X, w, dim, eps, Xn, range);
+	}
+	HIPCHK(hipGetLastError());
+	return YALM_OK;
+}
+int launch_rmsnorm(bool split, const PfForms &f, const float *X, const float *w, int dim, int T, float eps, uint16_t *Xn,
+                   unsigned *range, hipStream_t st) {
+	return split ? launch_rmsnorm_t<true>(f, X, w, dim, T, eps, Xn, range, st)
+	             : launch_rmsnorm_t<false>(f, X, w, dim, T, eps, Xn, range, st);
+}
+
 template <int D, bool SPLIT>
 int launch_attn_prefill_t(const uint16_t *Q, const uint16_t *kc, const uint16_t *vc, int T, int pos0, int n_heads,
 						  int n_kv, uint16_t *O, hipStream_t st) {
@@ -481,8 +517,7 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp, const int 
 		// the k | v columns' (their cache rows then carry one f16 rounding, infer.cpp:299)
 		unsigned *rg = b.range + (size_t)l * RG_N;
 		const int he = hexp ? hexp[l] : 0;
-		pf::rmsnorm_rows_kernel<true><<<T, 256, 0, st>>>(b.X, w.rms_att, c.dim, c.norm_eps, b.Xn, rg + RG_XATT);
-		HIPCHK(hipGetLastError());
+		TRY(launch_rmsnorm(true, f, b.X, w.rms_att, c.dim, T, c.norm_eps, b.Xn, rg + RG_XATT, st));
 		{
 			pf::BSrc qkv{};
 			qkv.p[0] = (const uint16_t *)w.wq;
@@ -544,11 +579,7 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp, const int 
 				TRY(launch_plain(f, bn_wo, b.O, sp * q_dim, T, sp * q_dim, q_dim, one(w.wo, c.dim), c.dim, e, st));
 			}
 		}
-		if (split)
-			pf::rmsnorm_rows_kernel<true><<<T, 256, 0, st>>>(b.X, w.rms_ffn, c.dim, c.norm_eps, b.Xn, rg + RG_XFFN);
-		else
-			pf::rmsnorm_rows_kernel<false><<<T, 256, 0, st>>>(b.X, w.rms_ffn, c.dim, c.norm_eps, b.Xn, rg + RG_XFFN);
-		HIPCHK(hipGetLastError());
+		TRY(launch_rmsnorm(split, f, b.X, w.rms_ffn, c.dim, T, c.norm_eps, b.Xn, rg + RG_XFFN, st));
 		const float hscale = ldexpf(1.0f, -he);
 		if (small) {
 			const pf::BRowsGlu<64> bm{(const uint16_t *)w.w1, (const uint16_t *)w.w3};
@@ -585,13 +616,8 @@ int enqueue_prefill(yalm_decoder_s *d, int T, int pos0, bool want_lp, const int 
 	}
 	if (!want_lp)
 		return YALM_OK;
-	if (split)
-		pf::rmsnorm_rows_kernel<true><<<T, 256, 0, st>>>(b.X, d->rms_final, c.dim, c.norm_eps, b.Xn,
-                                                         b.range + (size_t)c.n_layers * RG_N + RG_XATT);
-	else
-		pf::rmsnorm_rows_kernel<false><<<T, 256, 0, st>>>(b.X, d->rms_final, c.dim, c.norm_eps, b.Xn,
-                                                          b.range + (size_t)c.n_layers * RG_N + RG_XATT);
-	HIPCHK(hipGetLastError());
+	TRY(launch_rmsnorm(split, f, b.X, d->rms_final, c.dim, T, c.norm_eps, b.Xn,
+	                   b.range + (size_t)c.n_layers * RG_N + RG_XATT, st));
 	const int cls_bn = pick_bn(f, PG_CLS, T, c.vocab_size, false);
 	const int ntiles = cls_bn ? c.vocab_size / cls_bn : 1;
 	pf::E16Logits e;
