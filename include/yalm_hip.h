@@ -197,7 +197,8 @@ int yalm_decoder_set_launch(yalm_decoder d, int flags);
 int yalm_attn_wo_plan(const yalm_config *config, int slots, int *splits, int *grid);
 /* Timeline of the most recent fused attention + Wo launch (decoder created with
  * YALM_ATTN_WO_TRACE=1): 16 stamps per workgroup at [w * 16 + k]: k < 8
- * s_memrealtime (100 MHz), k + 8 the shader clock (s_memtime) at the same point; k = 0 start, 1 hand-off signalled (attention; 0 if this workgroup did not
+ * s_memrealtime (100 MHz), k + 8 the shader clock (s_memtime) at the same point (k = 0: instead the
+ * workgroup's place, HW_ID | XCC_ID << 32); k = 0 start, 1 hand-off signalled (attention; 0 if this workgroup did not
  * finish a kv head) or Wo slice landed (Wo; the trace waits for it), 2 poll passed (Wo) or
  * first K/V/q loads landed (attention; the trace waits for them), 3 end; attention units:
  * 4 scores of the last chunk, 5 its softmax, 6 P.V sums combined, 7 head outputs / partials

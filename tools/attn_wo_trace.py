@@ -74,7 +74,7 @@ def main():
         print(f"  {name:18s} med {np.median(dt):6.2f} max {dt.max():6.2f} us  {np.median(dc):8.0f} shader clocks"
               f"  ({np.median(dc) / np.maximum(np.median(dt), 1e-3) / 1e3:5.2f} GHz)")
 
-    for k0, k1, name in ((0, 2, "start->loads"), (2, 4, "loads->last scores"), (4, 5, "scores->softmax"),
+    for k0, k1, name in ((2, 4, "loads->last scores"), (4, 5, "scores->softmax"),
                          (5, 6, "softmax->P.V"), (6, 7, "P.V->issued")):
         phase(a_tr, a_clk, k0, k1, name)
     if mer_m.any():
@@ -91,6 +91,29 @@ def main():
         print(f"  last partial issued {last_part:6.2f} us; last partial seen {mergers[:, 7].max():6.2f} us; "
               f"last head {mergers[:, 1].max():6.2f} us")
     print(f"head signalled   {q(writers[:, 1])}  ({len(writers)} writers)")
+    # where each workgroup ran (slot 8: HW_ID | XCC_ID << 32): CU = (XCC, SE, SH, CU id)
+    hw = clk[:, 0].astype(np.uint64)
+    hwid, xcc = (hw & 0xFFFFFFFF).astype(np.int64), (hw >> np.uint64(32)).astype(np.int64) & 0xF
+    cu_key = xcc * 4096 + ((hwid >> 13) & 0x7) * 256 + ((hwid >> 12) & 1) * 16 + ((hwid >> 8) & 0xF)
+    wo_keys = cu_key[na:]
+    wo_per_cu = {}
+    for k_ in wo_keys:
+        wo_per_cu[k_] = wo_per_cu.get(k_, 0) + 1
+    heads_cu = cu_key[:na][tr[:na, 1] > 0]
+    share = [wo_per_cu.get(k_, 0) for k_ in heads_cu]
+    print(f"placement: {len(set(cu_key.tolist()))} distinct CUs; Wo workgroups on {len(wo_per_cu)} CUs "
+          f"(per CU: {sorted(set(wo_per_cu.values()))}); head writers' CUs host "
+          f"{np.bincount(share).tolist() if share else []} Wo workgroups (count of writers with 0, 1, 2, ..)")
+    # which Wo workgroup shares each head writer's CU (workgroup index b of the writer, j of the Wo)
+    wo_of_cu = {k_: j for j, k_ in enumerate(wo_keys.tolist())}
+    pairs = [(int(b), wo_of_cu.get(int(cu_key[b]), -1)) for b in np.nonzero(tr[:na, 1] > 0)[0]]
+    print(f"  head writer b -> co-resident Wo j: {pairs[:12]}{' ...' if len(pairs) > 12 else ''}; "
+          f"j == b for {sum(1 for b, j in pairs if j == b)} of {len(pairs)}")
+    wo_ex = wo[:, 3]
+    on_head_cu = np.array([k_ in set(heads_cu.tolist()) for k_ in wo_keys])
+    if on_head_cu.any():
+        print(f"  Wo end on head CUs {q(wo_ex[on_head_cu])}; elsewhere {q(wo_ex[~on_head_cu])}")
+        print(f"  Wo poll passed on head CUs {q(wo[on_head_cu, 2])}; elsewhere {q(wo[~on_head_cu, 2])}")
     print(f"Wo start         {q(wo[:, 0])}")
     print(f"Wo slice landed  {q(wo[:, 1])}")
     print(f"Wo poll passed   {q(wo[:, 2])}")

@@ -205,8 +205,11 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_wo_kernel(const float *__re
 	// (kept in registers, stored when the workgroup is done: see attention.h `stamp`)
 	unsigned long long *tr = p.trace && tid == 0 ? p.trace + (size_t)b * AWO_TRACE_N : nullptr;
 	unsigned long long t_start = 0, c_start = 0;
-	if (tr)
-		t_start = __builtin_amdgcn_s_memrealtime(), c_start = __builtin_amdgcn_s_memtime();
+	if (tr) { // slot 8 (the start's shader clock) carries where the workgroup runs: HW_ID | XCC_ID << 32
+		t_start = __builtin_amdgcn_s_memrealtime();
+		c_start = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+		          ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);
+	}
 
 	const unsigned epoch = step->epoch; // this launch's tag (step_begin_kernel / set_step_full_kernel)
 	if (b < munits) { // ---- attention or merger workgroup
