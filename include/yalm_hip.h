@@ -303,7 +303,8 @@ int yalm_prefill_time(yalm_decoder d, int n, int iters, float *avg_ms);
  * defaults: qkv|wo|glu|w2|cls|test:<128|192|256|320> force that GEMM's tile width;
  * 8p:0 the 2-phase kernel; persist:0 one workgroup per tile; skinny:0 the large tiles
  * for T <= 64 too; qkv1:0 the q and k|v GEMMs as two launches; skl:0 the skinny GEMMs'
- * weights as register loads. Every form is exact against the others (tests). An
+ * weights as register loads; wnorm:0 the row norms as one workgroup per row (default:
+ * one wave per row). Every GEMM form is exact against the others (tests). An
  * unknown key is YALM_ERR_ARG. */
 int yalm_set_prefill_forms(yalm_decoder d, const char *spec);
 
