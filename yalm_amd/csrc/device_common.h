@@ -27,6 +27,8 @@ struct StepState {
 	                // (set_step_full_kernel); in-launch hand-off flags carry it, so they never need a reset
 	unsigned xbase; // IPC tensor parallelism (tp_exchange.h): this launch sequence's first exchange index
 	unsigned xnext; // the next sequence's (xbase + the exchanges this one uses)
+	float rope[256]; // (cos, sin) of pos * inv_freq[j], j < head_dim / 2 (infer.cpp:291-301), once per
+	                 // step (step_begin_kernel / set_step_full_kernel) for the QKV GEMV's epilogue
 };
 
 // Cross-lane exchange without the LDS crossbar: __shfl_xor lowers to

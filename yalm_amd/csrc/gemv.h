@@ -182,10 +182,9 @@ struct PQKV {
 			return;
 		}
 		int i = vr < q_dim ? vr : vr - q_dim;
-		float freq = inv_freq[(i % head_dim) >> 1];
-		float val = (float)step->pos * freq;
-		float fcr = cosf(val);
-		float fci = sinf(val);
+		const int j = (i % head_dim) >> 1; // cos / sin of pos * inv_freq[j]: the step kernel's table
+		float fcr = step->rope[2 * j];
+		float fci = step->rope[2 * j + 1];
 		float r0 = v0 * fcr - v1 * fci;
 		float r1 = v0 * fci + v1 * fcr;
 		if (vr < q_dim) {

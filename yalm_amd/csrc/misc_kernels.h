@@ -16,9 +16,25 @@ __global__ void set_step_kernel(StepState *st, int token, int pos, int reset_gen
 		st->n_gen = 0;
 }
 
+// RoPE (cos, sin) of this step's position: the angles the QKV epilogue used to compute itself
+// with cosf / sinf on one lane per row pair at its tail (infer.cpp:291-301, the same expression,
+// so the same values), now once per step by the step kernel's threads.
+__device__ __forceinline__ void step_rope(StepState *st, int pos, const float *__restrict__ inv_freq, int half) {
+	for (int j = threadIdx.x; j < half; j += blockDim.x) {
+		const float val = (float)pos * inv_freq[j];
+		st->rope[2 * j] = cosf(val);
+		st->rope[2 * j + 1] = sinf(val);
+	}
+}
+
 // Explicit indices for the per-block test hook (Block::block signature); n_ex: the IPC
 // tensor-parallel exchanges the block uses (tp_exchange.h).
-__global__ void set_step_full_kernel(StepState *st, int pos, int kv_sink, int kv_pos, int kv_len, int n_ex = 0) {
+__global__ void set_step_full_kernel(StepState *st, int pos, int kv_sink, int kv_pos, int kv_len, int n_ex = 0,
+                                     const float *__restrict__ inv_freq = nullptr, int half = 0) {
+	if (inv_freq)
+		step_rope(st, pos, inv_freq, half);
+	if (threadIdx.x != 0)
+		return;
 	st->pos = pos;
 	st->kv_sink = kv_sink;
 	st->kv_pos = kv_pos;
@@ -41,9 +57,11 @@ __global__ void epoch_bump_kernel(StepState *st, int n_ex) {
 // n_ex: the IPC tensor-parallel exchanges this forward uses (tp_exchange.h).
 template <class WT>
 __global__ __launch_bounds__(256) void step_begin_kernel(StepState *st, const void *__restrict__ emb, int dim,
-                                                         float *__restrict__ x, int max_seq_len, int n_ex) {
+                                                         float *__restrict__ x, int max_seq_len, int n_ex,
+                                                         const float *__restrict__ inv_freq, int half) {
 	const int token = st->token;
 	const int pos = st->pos;
+	step_rope(st, pos, inv_freq, half);
 	const char *row = (const char *)emb + (size_t)token * dim * WT::BYTES;
 	for (int i = threadIdx.x * WT::EPL; i < dim; i += blockDim.x * WT::EPL) {
 		float f[WT::EPL];

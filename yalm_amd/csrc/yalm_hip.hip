@@ -782,7 +782,8 @@ static int enqueue_logits_t(yalm_decoder_s *d, int consume_ex, int push_ex) {
 
 template <class WT>
 static int enqueue_begin_t(yalm_decoder_s *d, int n_ex) {
-	step_begin_kernel<WT><<<1, 256, 0, d->stream>>>(d->step, d->emb, d->c.dim, d->x, d->c.max_seq_len, n_ex);
+	step_begin_kernel<WT><<<1, 256, 0, d->stream>>>(d->step, d->emb, d->c.dim, d->x, d->c.max_seq_len, n_ex,
+	                                                 d->inv_freq, d->c.head_dim / 2);
 	HIPCHK(hipGetLastError());
 	return YALM_OK;
 }
@@ -1318,7 +1319,8 @@ extern "C" int yalm_block(yalm_decoder d, int layer, int pos, int kv_sink, int k
 	ARGCHK(d && layer >= 0 && layer < d->c.n_layers, "bad layer");
 	ARGCHK(kv_len >= 1 && kv_len <= d->c.max_seq_len && kv_pos >= 0 && kv_pos < d->c.max_seq_len,
 	       "bad kv indices");
-	set_step_full_kernel<<<1, 1, 0, d->stream>>>(d->step, pos, kv_sink, kv_pos, kv_len, d->ipc ? 2 : 0);
+	set_step_full_kernel<<<1, 64, 0, d->stream>>>(d->step, pos, kv_sink, kv_pos, kv_len, d->ipc ? 2 : 0, d->inv_freq,
+	                                              d->c.head_dim / 2);
 	HIPCHK(hipGetLastError());
 	TRY(DISPATCH_WT(d->c.weight_dtype, enqueue_layer_t, d, layer, 0, false, true));
 	if (d->ipc) { // the layer's W2 pushed its partial: collect the sum into x (a forward's next GEMV would)
