@@ -29,6 +29,8 @@ struct StepState {
 	unsigned xnext; // the next sequence's (xbase + the exchanges this one uses)
 	float rope[256]; // (cos, sin) of pos * inv_freq[j], j < head_dim / 2 (infer.cpp:291-301), once per
 	                 // step (step_begin_kernel / set_step_full_kernel) for the QKV GEMV's epilogue
+	float rope_sink[256]; // (cos, sin) of 1 * inv_freq[j]: the sink keys' one-position rotation
+	                      // (infer.cpp:303-317), written beside rope
 };
 
 // Cross-lane exchange without the LDS crossbar: __shfl_xor lowers to

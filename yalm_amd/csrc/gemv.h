@@ -81,6 +81,21 @@ struct PResidual {
 
 // policies with a pre(g, r) / finish_pre epilogue (PRE = true)
 template <class P, class = void>
+struct gemv_early : std::false_type {};
+template <class P>
+struct gemv_early<P, std::void_t<decltype(P::EARLY)>> : std::bool_constant<P::EARLY> {};
+
+struct NoEarly {};
+template <class P, bool = gemv_early<P>::value>
+struct early_of {
+	using type = NoEarly;
+};
+template <class P>
+struct early_of<P, true> {
+	using type = typename P::Early;
+};
+
+template <class P, class = void>
 struct gemv_pre : std::false_type {};
 template <class P>
 struct gemv_pre<P, std::void_t<decltype(P::PRE)>> : std::bool_constant<P::PRE> {};
@@ -156,8 +171,45 @@ struct PQKV {
 	const StepState *step;
 	float *q_out;
 	uint16_t *kcache, *vcache;
-	// workgroup 0 rotates the attention sinks (see rotate_sinks below)
-	__device__ __forceinline__ void prologue() const;
+	// the attention sinks' one-position rotation (infer.cpp:303-317, infer.cu:679-697), spread over
+	// the launch: each thread of every workgroup loads its pair of rows < KV_SINKS BEFORE the weight
+	// stream (early, unconditionally: step->kv_sink is not known yet) and rotates it after the stream
+	// (late), so no wave waits on a dependent round trip; rows < kv_sink never alias the kv_pos
+	// row the epilogue writes (kv_pos >= kv_sink)
+	static constexpr bool EARLY = true;
+	static constexpr int KV_SINKS = 2; // model.h:12
+	struct Early {
+		uint32_t kv; // the pair (fp16 x 2) of pair index pi below
+		int pi;
+	};
+	__device__ __forceinline__ Early early() const {
+		Early e;
+		e.pi = (int)(threadIdx.x * gridDim.x + blockIdx.x);
+		const int half = kv_dim >> 1;
+		e.kv = e.pi < KV_SINKS * half ? *(const uint32_t *)(kcache + (size_t)(e.pi / half) * kv_dim + 2 * (e.pi % half))
+		                              : 0u;
+		return e;
+	}
+	__device__ __forceinline__ void rotate_pair(int pi, uint32_t kv) const {
+		const int half = kv_dim >> 1;
+		const int r = pi / half, i = 2 * (pi % half);
+		float v0 = h2f((uint16_t)(kv & 0xFFFF)), v1 = h2f((uint16_t)(kv >> 16));
+		const int j = (i % head_dim) >> 1;
+		float fcr = step->rope_sink[2 * j], fci = step->rope_sink[2 * j + 1];
+		const uint32_t o0 = f2h(v0 * fcr - v1 * fci), o1 = f2h(v0 * fci + v1 * fcr);
+		*(uint32_t *)(kcache + (size_t)r * kv_dim + i) = o0 | (o1 << 16);
+	}
+	__device__ __forceinline__ void late(const Early &e) const {
+		const int half = kv_dim >> 1, npairs = step->kv_sink * half;
+		const int stride = (int)(blockDim.x * gridDim.x);
+		for (int pi = e.pi; pi < npairs; pi += stride) { // past KV_SINKS rows (not in the reference's schedule): loaded here
+			const uint32_t kv = pi == e.pi && pi < KV_SINKS * half
+			                        ? e.kv
+			                        : *(const uint32_t *)(kcache + (size_t)(pi / half) * kv_dim + 2 * (pi % half));
+			rotate_pair(pi, kv);
+		}
+	}
+	__device__ __forceinline__ void prologue() const { late(early()); } // gemv_kernel
 	__device__ __forceinline__ const char *row(int g, int r) const {
 		int vr = 2 * g + r;
 		if (vr < q_dim)
@@ -216,33 +268,6 @@ struct PGlu {
 	}
 	__device__ __forceinline__ void finish_all(int g, const float *acc) const { finish(g, acc, 0); }
 };
-
-// Rotate the attention-sink keys by one position (infer.cpp:303-317,
-// infer.cu:679-697), executed by workgroup 0 of the QKV launch. Rows < kv_sink
-// never alias the kv_pos row being written (kv_pos >= kv_sink).
-__device__ __forceinline__ void rotate_sinks(uint16_t *kcache, int kv_sink, int kv_dim, int head_dim,
-                                             const float *inv_freq) {
-	for (int r = 0; r < kv_sink; ++r) {
-		for (int i = 2 * threadIdx.x; i < kv_dim; i += 2 * blockDim.x) {
-			size_t o = (size_t)r * kv_dim + i;
-			float v0 = h2f(kcache[o]), v1 = h2f(kcache[o + 1]);
-			float freq = inv_freq[(i % head_dim) >> 1];
-			float val = 1.0f * freq;
-			float fcr = cosf(val), fci = sinf(val);
-			kcache[o] = f2h(v0 * fcr - v1 * fci);
-			kcache[o + 1] = f2h(v0 * fci + v1 * fcr);
-		}
-	}
-}
-
-template <class WT>
-__device__ __forceinline__ void PQKV<WT>::prologue() const {
-	if (blockIdx.x == 0) {
-		const int kv_sink = step->kv_sink;
-		if (kv_sink > 0)
-			rotate_sinks(kcache, kv_sink, kv_dim, head_dim, inv_freq);
-	}
-}
 
 // Stage x (n floats) into LDS, optionally as rmsnorm(x) * w (infer.cpp:134-144
 // statement order: scale = 1/sqrt(sum/n + eps); o = x * scale * w).
@@ -538,13 +563,17 @@ __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__re
 		for (int r = 0; r < R; ++r)
 			xr[r] = p.pre(g0, r);
 	}
+	typename early_of<P>::type ek{}; // PQKV: the sink pairs, loaded ahead of the weight stream
+	if constexpr (gemv_early<P>::value)
+		ek = p.early();
 	u32x4_t buf[U];
 #pragma unroll
 	for (int u = 0; u < U; ++u) {
 		buf[u] = load_nt16(u < mine ? iaddr(ivr, ic) : dummy);
 		advance(ivr, ic);
 	}
-	p.prologue();
+	if constexpr (!gemv_early<P>::value)
+		p.prologue();
 	for (int i = threadIdx.x; i < ngl * R * W; i += THREADS)
 		part[i] = 0.0f;
 	if constexpr (TIN)
@@ -581,6 +610,8 @@ __global__ __launch_bounds__(THREADS) void gemv_rb_kernel(P p, const float *__re
 		if (lane == 0)
 			part[pslot(cur)] = s;
 	}
+	if constexpr (gemv_early<P>::value) // after the stream: its loads (and step's) have long landed
+		p.late(ek);
 	__syncthreads();
 	for (int gl = threadIdx.x; gl < ngl; gl += THREADS) {
 		float a[R];

@@ -24,6 +24,9 @@ __device__ __forceinline__ void step_rope(StepState *st, int pos, const float *_
 		const float val = (float)pos * inv_freq[j];
 		st->rope[2 * j] = cosf(val);
 		st->rope[2 * j + 1] = sinf(val);
+		const float val1 = 1.0f * inv_freq[j];
+		st->rope_sink[2 * j] = cosf(val1);
+		st->rope_sink[2 * j + 1] = sinf(val1);
 	}
 }
 
