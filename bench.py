@@ -159,7 +159,13 @@ def pmc_traffic(kernel_match):
     import glob
     import statistics
 
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_fetch_size*.csv")), reverse=True):
+    import re
+
+    def run_order(f):  # profile prefixes r<round><run letters>: r6w < r6ah (a < z < aa < ah, spreadsheet order)
+        m = re.match(r"r(\d+)([a-z]+)_", os.path.basename(f))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_fetch_size*.csv")), key=run_order, reverse=True):
         rows = list(csv.DictReader(open(f)))
         vals = [float(r["Counter_Value"]) for r in rows
                 if r["Counter_Name"] == "FETCH_SIZE" and all(k in r["Kernel_Name"] for k in kernel_match)]
